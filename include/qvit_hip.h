@@ -1,0 +1,165 @@
+/*
+ * qvit_hip.h — C-ABI of libqvit_hip.so, the MI355X (gfx950) implementation of the
+ * 4-bit QuantizeLinear / QuantizeConv2d forward path of LongAoTianxia/Quantized_ViT.
+ *
+ * Every entry point replaces one step of the reference's fake-quant forward
+ * (paths relative to the reference checkout; OTO = QViT_with_GETA/only_train_once):
+ *
+ *   qvit_quantize_act_i8      OTO/quantization/quant_layers.py:356-381 (QuantizeMixin.quantize_act)
+ *                             -> SymQuantizerLinear.forward :137-161 / SymQuantizerNonLinear.forward :41-69,
+ *                             emitted as integer codes k (value = d * k) instead of fake-quant floats;
+ *                             also 4-bit quantization/quant_ultra.py:59-73 (activation_quantize_fn).
+ *   qvit_fake_quant_f32       the same quantizers emitting the reference's fp32 fake-quant values
+ *                             (used when a layer's level count does not fit int8, e.g. num_bits > 8).
+ *   qvit_pack_weight          quant_layers.py:332-354 (QuantizeMixin.quantize_weight) + the GEMM operand
+ *                             layout: codes packed int4 (8 per u32) or int8, rows padded/permuted.
+ *   qvit_im2col_quant_i8      quant_layers.py:575-587 (QuantizeConv2d.forward): the conv input patches
+ *                             quantized to codes, K-order (c, kh, kw) = the reference weight flattening.
+ *   qvit_layernorm_quant_i8   vit_model.py:193,206-207 (Block.norm1/norm2, eps 1e-6) fused with the next
+ *                             QuantizeLinear's quantize_act (quant_layers.py:497-498).
+ *   qvit_gemm                 quant_layers.py:499 (nn.functional.linear on fake-quant operands) as an
+ *                             int8 x int4/int8 -> int32 MFMA contraction with a fused epilogue:
+ *                             d_act * d_wt * acc + bias, optionally + residual (vit_model.py:206-207),
+ *                             or GELU (vit_model.py:173) + the next layer's activation quantizer.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only. All pointers are device pointers (hipMalloc'd / torch CUDA
+ *     tensors) unless stated otherwise. Every entry point is stream-ordered on `stream`, never
+ *     synchronises the host, never allocates, and is safe to capture into a hipGraph.
+ *   - Quantizer parameters are per-tensor device scalars (float[1]): d_quant, q_m, t_quant, exactly the
+ *     reference's nn.Parameter([1]) tensors (quant_layers.py:315-325). t_quant may be NULL for the
+ *     linear quantizer. Reading them on the device keeps the host free of .item() syncs.
+ *   - Return value: 0 on success; QVIT_E* (< 0) on a rejected argument; QVIT_EHIP - hipError_t
+ *     when a launch fails. qvit_strerror() maps a code to text.
+ */
+#ifndef QVIT_HIP_H
+#define QVIT_HIP_H
+
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------------------------- */
+#define QVIT_OK          0
+#define QVIT_EINVAL     -1   /* bad size / stride / enum */
+#define QVIT_EALIGN     -2   /* pointer or leading dimension not aligned as required */
+#define QVIT_ENULL      -3   /* required pointer is NULL */
+#define QVIT_EHIP    -1000   /* QVIT_EHIP - (int)hipError_t */
+
+/* ---- quantizer kinds (QuantizationType, quant_layers.py:20-24; quant_ultra.py) ---------- */
+#define QVIT_QT_LINEAR      0  /* SymQuantizerLinear / DGEQuantizer forward: k = sgn(x) rne(|x|/d) */
+#define QVIT_QT_NONLINEAR   1  /* SymQuantizerNonLinear: k = sgn(x) rne(exp(t log|x|)/d)          */
+#define QVIT_QT_ULTRA_ACT   2  /* quant_ultra activation_quantize_fn: k = rne(clamp(x,0,1) (2^b-1)),
+                                  d_quant = NULL, the level count 2^b-1 is passed as `levels`      */
+
+/* ---- GEMM weight storage ---------------------------------------------------------------- */
+#define QVIT_W4 4   /* int4 codes, 8 per uint32 (see qvit_pack_weight for the nibble order) */
+#define QVIT_W8 8   /* int8 codes                                                           */
+
+/* ---- GEMM epilogues ----------------------------------------------------------------------- */
+#define QVIT_EPI_F32        0  /* C[m,n]  = d_act d_wt acc + bias[n]                 (fp32)          */
+#define QVIT_EPI_F32_RESID  1  /* C[m,n] += d_act d_wt acc + bias[n]                 (fp32, in place) */
+#define QVIT_EPI_I8_GELU    2  /* C[m,n]  = q_next(gelu(d_act d_wt acc + bias[n]))  (int8 codes)    */
+#define QVIT_EPI_I8         3  /* C[m,n]  = q_next(d_act d_wt acc + bias[n])        (int8 codes)    */
+#define QVIT_EPI_I32        4  /* C[m,n]  = acc                                      (int32, exact)  */
+
+/* Tile geometry the packed operands must be padded to. */
+#define QVIT_TILE_N  128   /* weight rows (out features) are padded to a multiple of this  */
+#define QVIT_TILE_K  128   /* the reduction dim is padded to a multiple of this (zeros)    */
+
+const char* qvit_strerror(int code);
+/* Library version / build tag, e.g. "qvit_hip 0.1 gfx950". Host pointer, static storage. */
+const char* qvit_version(void);
+
+/*
+ * Activation quantizer -> int8 codes (value = d_quant * code).
+ *   x      : fp32 [rows][ldx], first `cols` columns used
+ *   codes  : int8 [rows][ldc]; columns [cols, kpad) are written with 0 (kpad <= ldc, kpad % 16 == 0)
+ *   qtype  : QVIT_QT_*; levels is only read for QVIT_QT_ULTRA_ACT.
+ * Codes saturate at +-127 (the caller rejects layers whose level count exceeds 127).
+ * Replaces quant_layers.py:356-381 (+ :41-69 / :137-161) and quant_ultra.py:66-73.
+ */
+int qvit_quantize_act_i8(const float* x, int64_t rows, int64_t cols, int64_t ldx,
+                         int qtype, const float* d_quant, const float* q_m, const float* t_quant,
+                         int levels, int8_t* codes, int64_t ldc, int64_t kpad, hipStream_t stream);
+
+/*
+ * Fake-quant fp32 values exactly as the reference returns them (y = sgn(x) * (d * rne(...)),
+ * saturation and zero masks in the reference's order). Elementwise over n contiguous floats.
+ * Replaces SymQuantizerLinear/NonLinear.forward (quant_layers.py:41-69,137-161) when a layer's
+ * levels do not fit the integer path.
+ */
+int qvit_fake_quant_f32(const float* x, int64_t n, int qtype, const float* d_quant,
+                        const float* q_m, const float* t_quant, int levels, float* y,
+                        hipStream_t stream);
+
+/*
+ * Weight quantizer + GEMM operand packing (QuantizeMixin.quantize_weight, quant_layers.py:332-354).
+ *   w      : fp32 [n][ldw], first k columns used (nn.Linear weight [out,in]; a conv weight
+ *            [Cout,Cin,kh,kw] is passed as [Cout][Cin*kh*kw]).
+ *   wfmt   : QVIT_W4 -> packed uint32 [npad][kpad/8]; QVIT_W8 -> int8 [npad][kpad].
+ *            npad % QVIT_TILE_N == 0, kpad % QVIT_TILE_K == 0, npad >= n, kpad >= k; padding = 0.
+ *   Row order: within every 64-row group the two 2-bit fields of the row index are swapped
+ *   (packed row (r<<4)|(q<<2)|j holds weight row (q<<4)|(r<<2)|j) so that each GEMM lane ends up
+ *   owning 16 consecutive output features.  W4 nibble order inside each uint32 covering
+ *   k0..k0+7: byte b holds k0+b in bits [0,4) and k0+4+b in bits [4,8), two's complement.
+ *   overflow (int32[1], device, may be NULL): atomically set to 1 if any code does not fit wfmt.
+ */
+int qvit_pack_weight(const float* w, int64_t n, int64_t k, int64_t ldw, int qtype,
+                     const float* d_quant, const float* q_m, const float* t_quant, int wfmt,
+                     void* packed, int64_t npad, int64_t kpad, int32_t* overflow,
+                     hipStream_t stream);
+
+/*
+ * Pads a bias vector to npad floats (zeros past n; bias may be NULL -> all zeros).
+ */
+int qvit_pad_bias(const float* bias, int64_t n, float* out, int64_t npad, hipStream_t stream);
+
+/*
+ * Conv input -> quantized im2col codes for QuantizeConv2d (quant_layers.py:575-587), groups == 1.
+ *   x      : fp32 NCHW [B][C][H][W] contiguous
+ *   codes  : int8 [B*OH*OW][ldc], row (b, oh, ow), column (c, ih, iw) = c*kh*kw + ih*kw + iw;
+ *            columns [C*kh*kw, kpad) zero. Zero-padding of the image quantizes to code 0, as in
+ *            the reference (quantize_act runs before F.conv2d pads).
+ */
+int qvit_im2col_quant_i8(const float* x, int64_t B, int64_t C, int64_t H, int64_t W,
+                         int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw,
+                         int qtype, const float* d_quant, const float* q_m, const float* t_quant,
+                         int levels, int8_t* codes, int64_t ldc, int64_t kpad, hipStream_t stream);
+
+/*
+ * LayerNorm (biased variance, eps) followed by the next layer's activation quantizer.
+ *   x : fp32 [rows][ldx] (D = cols), gamma/beta fp32 [cols] (may be NULL -> 1 / 0)
+ *   codes : int8 [rows][ldc], columns [cols, kpad) zero.
+ */
+int qvit_layernorm_quant_i8(const float* x, int64_t rows, int64_t cols, int64_t ldx,
+                            const float* gamma, const float* beta, float eps,
+                            int qtype, const float* d_quant, const float* q_m,
+                            const float* t_quant, int levels,
+                            int8_t* codes, int64_t ldc, int64_t kpad, hipStream_t stream);
+
+/*
+ * Quantized contraction C = epilogue(A_codes @ W_codes^T).
+ *   A      : int8 codes [M][lda], K valid columns; K % QVIT_TILE_K == 0, lda % 16 == 0,
+ *            A 16-byte aligned, columns past the true in-features must be 0 (the quantizers
+ *            above write them so).
+ *   Wp     : packed weights from qvit_pack_weight (wfmt, npad rows, kpad == K).
+ *   N      : true out features (<= npad); outputs for n >= N are not written.
+ *   d_act, d_wt : device float[1] scales; bias : device float[npad] (padded) or NULL.
+ *   C      : fp32 / int8 / int32 [M][ldc] per epilogue; ldc % 4 == 0 (fp32/int32), % 16 (int8).
+ *   For QVIT_EPI_I8*: the next layer's quantizer (out_qtype, out_d, out_qm, out_t, out_levels).
+ */
+int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda,
+              const void* Wp, int wfmt, int64_t N, int64_t npad,
+              const float* d_act, const float* d_wt, const float* bias,
+              int epilogue, void* C, int64_t ldc,
+              int out_qtype, const float* out_d, const float* out_qm, const float* out_t,
+              int out_levels, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QVIT_HIP_H */

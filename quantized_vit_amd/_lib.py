@@ -1,0 +1,184 @@
+"""ctypes binding of libqvit_hip.so (include/qvit_hip.h) plus thin torch-tensor wrappers.
+
+This is the only place the Python side touches the C-ABI. There is no fallback: if the
+library is missing or a GPU is required and absent, calls raise. Tensors are passed as raw
+device pointers; every call is enqueued on torch's current HIP stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libqvit_hip.so")
+
+# ---- constants mirrored from include/qvit_hip.h ---------------------------------------------
+QT_LINEAR = 0
+QT_NONLINEAR = 1
+QT_ULTRA_ACT = 2
+QT_FORCE_CAREFUL = 0x100  # test-only: disable the guarded fast path
+
+W4 = 4
+W8 = 8
+
+EPI_F32 = 0
+EPI_F32_RESID = 1
+EPI_I8_GELU = 2
+EPI_I8 = 3
+EPI_I32 = 4
+
+TILE_N = 128
+TILE_K = 128
+
+_c_p = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int
+_f32 = ctypes.c_float
+
+# name -> argtypes (restype is int for all but the string getters)
+_SIGNATURES = {
+    "qvit_quantize_act_i8": [_c_p, _i64, _i64, _i64, _i32, _c_p, _c_p, _c_p, _i32, _c_p, _i64, _i64, _c_p],
+    "qvit_fake_quant_f32": [_c_p, _i64, _i32, _c_p, _c_p, _c_p, _i32, _c_p, _c_p],
+    "qvit_pack_weight": [_c_p, _i64, _i64, _i64, _i32, _c_p, _c_p, _c_p, _i32, _c_p, _i64, _i64, _c_p, _c_p],
+    "qvit_pad_bias": [_c_p, _i64, _c_p, _i64, _c_p],
+    "qvit_im2col_quant_i8": [_c_p, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32,
+                             _i32, _c_p, _c_p, _c_p, _i32, _c_p, _i64, _i64, _c_p],
+    "qvit_layernorm_quant_i8": [_c_p, _i64, _i64, _i64, _c_p, _c_p, _f32, _i32, _c_p, _c_p, _c_p, _i32,
+                                _c_p, _i64, _i64, _c_p],
+    "qvit_gemm": [_c_p, _i64, _i64, _i64, _c_p, _i32, _i64, _i64, _c_p, _c_p, _c_p, _i32, _c_p, _i64,
+                  _i32, _c_p, _c_p, _c_p, _i32, _c_p],
+}
+STRING_FUNCS = {"qvit_strerror": [_i32], "qvit_version": []}
+EXPORTED_SYMBOLS = sorted(list(_SIGNATURES) + list(STRING_FUNCS))
+
+_lock = threading.Lock()
+_lib: Optional[ctypes.CDLL] = None
+
+
+class QvitError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Loads libqvit_hip.so (no compute). Raises if it is absent: there is no fallback path."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise QvitError(
+                f"{path} is missing: build it with `python -m quantized_vit_amd.build` "
+                "(the HIP extension is required; there is no CPU fallback)")
+        lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        for name, args in _SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = ctypes.c_int
+        for name, args in STRING_FUNCS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = ctypes.c_char_p
+        _lib = lib
+        return lib
+
+
+def version() -> str:
+    return load().qvit_version().decode()
+
+
+def _check(code: int, what: str) -> None:
+    if code != 0:
+        msg = load().qvit_strerror(code).decode()
+        raise QvitError(f"{what} failed: {msg} (status {code})")
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _stream(dev: torch.device) -> int:
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _require_gpu(t: torch.Tensor, name: str) -> None:
+    if not t.is_cuda:
+        raise QvitError(f"{name} must be a ROCm device tensor (got {t.device}); the HIP path has no CPU fallback")
+
+
+# ---- wrappers -------------------------------------------------------------------------------
+def quantize_act_i8(x2d: torch.Tensor, qtype: int, d: Optional[torch.Tensor], qm: Optional[torch.Tensor],
+                    t: Optional[torch.Tensor], levels: int, out: torch.Tensor, kpad: int) -> torch.Tensor:
+    _require_gpu(x2d, "input")
+    assert x2d.dtype == torch.float32 and x2d.dim() == 2 and x2d.stride(1) == 1
+    rows, cols = x2d.shape
+    _check(load().qvit_quantize_act_i8(_ptr(x2d), rows, cols, x2d.stride(0), qtype, _ptr(d), _ptr(qm), _ptr(t),
+                                       levels, _ptr(out), out.stride(0), kpad, _stream(x2d.device)),
+           "qvit_quantize_act_i8")
+    return out
+
+
+def fake_quant_f32(x: torch.Tensor, qtype: int, d: Optional[torch.Tensor], qm: Optional[torch.Tensor],
+                   t: Optional[torch.Tensor], levels: int = 0) -> torch.Tensor:
+    _require_gpu(x, "input")
+    xc = x.contiguous().float()
+    y = torch.empty_like(xc)
+    _check(load().qvit_fake_quant_f32(_ptr(xc), xc.numel(), qtype, _ptr(d), _ptr(qm), _ptr(t), levels, _ptr(y),
+                                      _stream(x.device)), "qvit_fake_quant_f32")
+    return y
+
+
+def pack_weight(w2d: torch.Tensor, qtype: int, d: torch.Tensor, qm: torch.Tensor, t: Optional[torch.Tensor],
+                wfmt: int, npad: int, kpad: int, overflow: Optional[torch.Tensor]) -> torch.Tensor:
+    _require_gpu(w2d, "weight")
+    assert w2d.dtype == torch.float32 and w2d.stride(1) == 1
+    n, k = w2d.shape
+    nbytes = npad * kpad // 2 if wfmt == W4 else npad * kpad
+    packed = torch.empty(nbytes, dtype=torch.uint8, device=w2d.device)
+    _check(load().qvit_pack_weight(_ptr(w2d), n, k, w2d.stride(0), qtype, _ptr(d), _ptr(qm), _ptr(t), wfmt,
+                                   _ptr(packed), npad, kpad, _ptr(overflow), _stream(w2d.device)),
+           "qvit_pack_weight")
+    return packed
+
+
+def pad_bias(bias: Optional[torch.Tensor], n: int, npad: int, device: torch.device) -> torch.Tensor:
+    out = torch.empty(npad, dtype=torch.float32, device=device)
+    b = None if bias is None else bias.detach().contiguous().float()
+    _check(load().qvit_pad_bias(_ptr(b), n, _ptr(out), npad, _stream(device)), "qvit_pad_bias")
+    return out
+
+
+def im2col_quant_i8(x: torch.Tensor, kh: int, kw: int, sh: int, sw: int, ph: int, pw: int, dh: int, dw: int,
+                    qtype: int, d, qm, t, levels: int, out: torch.Tensor, kpad: int) -> torch.Tensor:
+    _require_gpu(x, "input")
+    assert x.dtype == torch.float32 and x.is_contiguous() and x.dim() == 4
+    B, C, H, W = x.shape
+    _check(load().qvit_im2col_quant_i8(_ptr(x), B, C, H, W, kh, kw, sh, sw, ph, pw, dh, dw, qtype, _ptr(d),
+                                       _ptr(qm), _ptr(t), levels, _ptr(out), out.stride(0), kpad,
+                                       _stream(x.device)), "qvit_im2col_quant_i8")
+    return out
+
+
+def layernorm_quant_i8(x2d: torch.Tensor, gamma: Optional[torch.Tensor], beta: Optional[torch.Tensor], eps: float,
+                       qtype: int, d, qm, t, levels: int, out: torch.Tensor, kpad: int) -> torch.Tensor:
+    _require_gpu(x2d, "input")
+    assert x2d.dtype == torch.float32 and x2d.stride(1) == 1
+    rows, cols = x2d.shape
+    _check(load().qvit_layernorm_quant_i8(_ptr(x2d), rows, cols, x2d.stride(0), _ptr(gamma), _ptr(beta), eps, qtype,
+                                          _ptr(d), _ptr(qm), _ptr(t), levels, _ptr(out), out.stride(0), kpad,
+                                          _stream(x2d.device)), "qvit_layernorm_quant_i8")
+    return out
+
+
+def gemm(A: torch.Tensor, M: int, K: int, packed: torch.Tensor, wfmt: int, N: int, npad: int,
+         d_act: Optional[torch.Tensor], d_wt: Optional[torch.Tensor], bias_pad: Optional[torch.Tensor],
+         epilogue: int, C: torch.Tensor, out_qtype: int = 0, out_d=None, out_qm=None, out_t=None,
+         out_levels: int = 0) -> torch.Tensor:
+    _require_gpu(A, "codes")
+    _check(load().qvit_gemm(_ptr(A), M, K, A.stride(0), _ptr(packed), wfmt, N, npad, _ptr(d_act), _ptr(d_wt),
+                            _ptr(bias_pad), epilogue, _ptr(C), C.stride(0), out_qtype, _ptr(out_d), _ptr(out_qm),
+                            _ptr(out_t), out_levels, _stream(A.device)), "qvit_gemm")
+    return C

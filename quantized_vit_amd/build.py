@@ -1,0 +1,94 @@
+"""Builds libqvit_hip.so (gfx950) in-tree with hipcc: one object per .hip, one shared library.
+
+Usage: python -m quantized_vit_amd.build [--force] [--verbose]
+The library is written next to this file so it travels to the GPU box with the repo snapshot.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import shutil
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+INCLUDE = os.path.join(os.path.dirname(HERE), "include")
+BUILD = os.path.join(HERE, "_build")
+LIB = os.path.join(HERE, "libqvit_hip.so")
+ARCH = "gfx950"
+
+SOURCES = ["quant_kernels.hip", "gemm_w4a8.hip"]
+HEADERS = ["qvit_common.h"]
+
+HIPCC_FLAGS = [
+    f"--offload-arch={ARCH}",
+    "-O3",
+    "-fPIC",
+    "-std=c++17",
+    "-Wall",
+    "-Wno-unused-function",
+    "-fno-gpu-rdc",
+    # keep IEEE fp32 division/sqrt: the quantizer's careful path depends on it
+    "-fhip-fp32-correctly-rounded-divide-sqrt",
+]
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: the HIP extension cannot be built")
+
+
+def _newest_input_mtime() -> float:
+    paths = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
+    paths.append(os.path.join(INCLUDE, "qvit_hip.h"))
+    paths.append(os.path.abspath(__file__))
+    return max(os.path.getmtime(p) for p in paths)
+
+
+def is_stale() -> bool:
+    return not os.path.exists(LIB) or os.path.getmtime(LIB) < _newest_input_mtime()
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not is_stale():
+        return LIB
+    hipcc = _hipcc()
+    os.makedirs(BUILD, exist_ok=True)
+
+    def compile_one(src: str) -> str:
+        obj = os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
+        cmd = [hipcc, *HIPCC_FLAGS, "-I", INCLUDE, "-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"hipcc failed on {src}:\n{res.stdout}\n{res.stderr}")
+        if verbose and res.stderr.strip():
+            print(res.stderr, file=sys.stderr)
+        return obj
+
+    with ThreadPoolExecutor(max_workers=min(4, len(SOURCES))) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
+    tmp = LIB + ".tmp"
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"link failed:\n{res.stdout}\n{res.stderr}")
+    os.replace(tmp, LIB)
+    return LIB
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--verbose", action="store_true")
+    a = ap.parse_args()
+    print(build(force=a.force, verbose=a.verbose))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,402 @@
+// Memory-bound quantizer kernels of libqvit_hip.so (gfx950):
+//   activation -> int8 codes, fp32 fake-quant, weight -> packed int4/int8 operand,
+//   conv im2col -> codes, LayerNorm -> codes, bias padding.
+// Every kernel reads its fp32 input once and writes int8 once (16 B per lane where the layout
+// allows), so the bound is HBM bandwidth: 5 bytes moved per element.
+#include "qvit_common.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+inline int grid_for(int64_t work, int threads) {
+  int64_t g = cdiv(work, threads);
+  const int64_t cap = 256 * 16;  // 16 blocks per CU, grid-stride beyond
+  return (int)(g < cap ? (g > 0 ? g : 1) : cap);
+}
+
+// ---- activation quantizer: one thread = 16 columns of one row -> one 16-byte store ----------
+__global__ __launch_bounds__(kThreads) void quantize_act_kernel(
+    const float* __restrict__ x, int64_t rows, int64_t cols, int64_t ldx, int qtype,
+    const float* d, const float* qm, const float* t, int levels, int8_t* __restrict__ codes,
+    int64_t ldc, int64_t kpad) {
+  const QParams p = load_qparams(qtype, d, qm, t, levels);
+  const int64_t chunks_per_row = kpad / 16;
+  const int64_t total = rows * chunks_per_row;
+  const bool vec = ((ldx & 3) == 0) && ((((uintptr_t)x) & 15) == 0);
+  for (int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; id < total;
+       id += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = id / chunks_per_row;
+    const int64_t c0 = (id - r * chunks_per_row) * 16;
+    const float* src = x + r * ldx + c0;
+    float v[16];
+    if (vec && c0 + 16 <= cols) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float4 f = *reinterpret_cast<const float4*>(src + 4 * i);
+        v[4 * i + 0] = f.x; v[4 * i + 1] = f.y; v[4 * i + 2] = f.z; v[4 * i + 3] = f.w;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = (c0 + i < cols) ? src[i] : 0.f;
+    }
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      uint32_t acc = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int8_t k = to_i8_sat(quant_code(v[4 * i + b], p));
+        acc |= ((uint32_t)(uint8_t)k) << (8 * b);
+      }
+      w[i] = acc;
+    }
+    *reinterpret_cast<uint4*>(codes + r * ldc + c0) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void fake_quant_kernel(const float* __restrict__ x, int64_t n,
+                                                              int qtype, const float* d,
+                                                              const float* qm, const float* t,
+                                                              int levels, float* __restrict__ y) {
+  const QParams p = load_qparams(qtype, d, qm, t, levels);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    y[i] = fake_quant_value(x[i], p);
+  }
+}
+
+// ---- weight quantizer + operand packing ------------------------------------------------------
+// Packed row rho holds weight row perm(rho): inside each 64-row group swap bits [3:2] and [5:4].
+__device__ __forceinline__ int64_t perm_row(int64_t rho) {
+  const int64_t lo = rho & 3, r = (rho >> 2) & 3, q = (rho >> 4) & 3;
+  return (rho & ~int64_t(63)) | (r << 4) | (q << 2) | lo;
+}
+
+template <int WFMT>
+__global__ __launch_bounds__(kThreads) void pack_weight_kernel(
+    const float* __restrict__ w, int64_t n, int64_t k, int64_t ldw, int qtype, const float* d,
+    const float* qm, const float* t, void* __restrict__ packed, int64_t npad, int64_t kpad,
+    int32_t* overflow) {
+  const QParams p = load_qparams(qtype, d, qm, t, 0);
+  // one thread = 8 consecutive k of one packed row
+  const int64_t words_per_row = kpad / 8;
+  const int64_t total = npad * words_per_row;
+  for (int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; id < total;
+       id += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t rho = id / words_per_row;
+    const int64_t k0 = (id - rho * words_per_row) * 8;
+    const int64_t row = perm_row(rho);
+    int kc[8];
+    bool bad = false;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float v = 0.f;
+      if (row < n && k0 + i < k) v = w[row * ldw + k0 + i];
+      const float c = quant_code(v, p);
+      const float lim_lo = (WFMT == QVIT_W4) ? -8.f : -128.f;
+      const float lim_hi = (WFMT == QVIT_W4) ? 7.f : 127.f;
+      bad |= !(c >= lim_lo && c <= lim_hi);
+      kc[i] = (int)fminf(fmaxf(c, lim_lo), lim_hi);
+    }
+    if (bad && overflow) atomicOr(overflow, 1);
+    if (WFMT == QVIT_W4) {
+      uint32_t word = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        word |= ((uint32_t)(kc[b] & 0xF)) << (8 * b);
+        word |= ((uint32_t)(kc[b + 4] & 0xF)) << (8 * b + 4);
+      }
+      reinterpret_cast<uint32_t*>(packed)[rho * words_per_row + k0 / 8] = word;
+    } else {
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        lo |= ((uint32_t)(uint8_t)(int8_t)kc[b]) << (8 * b);
+        hi |= ((uint32_t)(uint8_t)(int8_t)kc[b + 4]) << (8 * b);
+      }
+      uint2* dst = reinterpret_cast<uint2*>(reinterpret_cast<int8_t*>(packed) + rho * kpad + k0);
+      *dst = make_uint2(lo, hi);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void pad_bias_kernel(const float* __restrict__ bias, int64_t n,
+                                                            float* __restrict__ out, int64_t npad) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < npad;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    out[i] = (bias != nullptr && i < n) ? bias[i] : 0.f;
+  }
+}
+
+// ---- conv input -> im2col codes ----------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void im2col_quant_kernel(
+    const float* __restrict__ x, int64_t B, int64_t C, int64_t H, int64_t W, int kh, int kw,
+    int sh, int sw, int ph, int pw, int dh, int dw, int64_t OH, int64_t OW, int qtype,
+    const float* d, const float* qm, const float* t, int levels, int8_t* __restrict__ codes,
+    int64_t ldc, int64_t kpad) {
+  const QParams p = load_qparams(qtype, d, qm, t, levels);
+  const int64_t K = C * kh * kw;
+  const int64_t chunks_per_row = kpad / 16;
+  const int64_t rows = B * OH * OW;
+  const int64_t total = rows * chunks_per_row;
+  // patchify fast path: a 16-wide chunk is 16 consecutive pixels of one input row
+  const bool patch16 = (kw % 16 == 0) && dw == 1 && pw == 0 && ph == 0 && (W % 4 == 0) &&
+                       (sw % 4 == 0) && ((((uintptr_t)x) & 15) == 0);
+  for (int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; id < total;
+       id += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = id / chunks_per_row;
+    const int64_t c0 = (id - r * chunks_per_row) * 16;
+    const int64_t b = r / (OH * OW);
+    const int64_t rem = r - b * OH * OW;
+    const int64_t oh = rem / OW, ow = rem - (rem / OW) * OW;
+    float v[16];
+    if (patch16 && c0 + 16 <= K) {
+      const int64_t ci = c0 / (kh * kw);
+      const int64_t r2 = c0 - ci * kh * kw;
+      const int64_t ih = r2 / kw, iw = r2 - ih * kw;
+      const int64_t y = oh * sh + ih * dh;
+      const int64_t xx = ow * sw + iw;
+      const float* src = x + ((b * C + ci) * H + y) * W + xx;
+      if (y < H && xx + 16 <= W) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float4 f = *reinterpret_cast<const float4*>(src + 4 * i);
+          v[4 * i + 0] = f.x; v[4 * i + 1] = f.y; v[4 * i + 2] = f.z; v[4 * i + 3] = f.w;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = (y < H && xx + i < W) ? src[i] : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int64_t kk = c0 + i;
+        float val = 0.f;
+        if (kk < K) {
+          const int64_t ci = kk / (kh * kw);
+          const int64_t r2 = kk - ci * kh * kw;
+          const int64_t ih = r2 / kw, iw = r2 - ih * kw;
+          const int64_t y = oh * sh - ph + ih * dh;
+          const int64_t xx = ow * sw - pw + iw * dw;
+          if (y >= 0 && y < H && xx >= 0 && xx < W) val = x[((b * C + ci) * H + y) * W + xx];
+        }
+        v[i] = val;
+      }
+    }
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      uint32_t acc = 0;
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb) {
+        const int8_t k = to_i8_sat(quant_code(v[4 * i + bb], p));
+        acc |= ((uint32_t)(uint8_t)k) << (8 * bb);
+      }
+      w[i] = acc;
+    }
+    *reinterpret_cast<uint4*>(codes + r * ldc + c0) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+// ---- LayerNorm + quantizer: one wave per row ----------------------------------------------------
+QVIT_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(kThreads) void layernorm_quant_kernel(
+    const float* __restrict__ x, int64_t rows, int64_t cols, int64_t ldx,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, int qtype,
+    const float* d, const float* qm, const float* t, int levels, int8_t* __restrict__ codes,
+    int64_t ldc, int64_t kpad) {
+  const QParams p = load_qparams(qtype, d, qm, t, levels);
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const bool vec = ((cols & 3) == 0) && ((ldx & 3) == 0) && ((((uintptr_t)x) & 15) == 0);
+  for (int64_t r = wave; r < rows; r += nwaves) {
+    const float* xr = x + r * ldx;
+    float s = 0.f;
+    if (vec) {
+      for (int64_t c = lane * 4; c < cols; c += 256) {
+        float4 f = *reinterpret_cast<const float4*>(xr + c);
+        s += (f.x + f.y) + (f.z + f.w);
+      }
+    } else {
+      for (int64_t c = lane; c < cols; c += 64) s += xr[c];
+    }
+    const float mean = wave_sum(s) / (float)cols;
+    float s2 = 0.f;
+    if (vec) {
+      for (int64_t c = lane * 4; c < cols; c += 256) {
+        float4 f = *reinterpret_cast<const float4*>(xr + c);
+        const float a = f.x - mean, b = f.y - mean, cc = f.z - mean, dd = f.w - mean;
+        s2 += (a * a + b * b) + (cc * cc + dd * dd);
+      }
+    } else {
+      for (int64_t c = lane; c < cols; c += 64) {
+        const float a = xr[c] - mean;
+        s2 += a * a;
+      }
+    }
+    const float var = wave_sum(s2) / (float)cols;
+    const float rstd = 1.0f / sqrtf(var + eps);
+    int8_t* cr = codes + r * ldc;
+    if (vec) {
+      for (int64_t c = lane * 4; c < cols; c += 256) {
+        float4 f = *reinterpret_cast<const float4*>(xr + c);
+        float vv[4] = {f.x, f.y, f.z, f.w};
+        uint32_t word = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float y = (vv[i] - mean) * rstd;
+          if (gamma) y = y * gamma[c + i];
+          if (beta) y = y + beta[c + i];
+          word |= ((uint32_t)(uint8_t)to_i8_sat(quant_code(y, p))) << (8 * i);
+        }
+        *reinterpret_cast<uint32_t*>(cr + c) = word;
+      }
+    } else {
+      for (int64_t c = lane; c < cols; c += 64) {
+        float y = (xr[c] - mean) * rstd;
+        if (gamma) y = y * gamma[c];
+        if (beta) y = y + beta[c];
+        cr[c] = to_i8_sat(quant_code(y, p));
+      }
+    }
+    for (int64_t c = cols + lane; c < kpad; c += 64) cr[c] = 0;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* qvit_strerror(int code) {
+  switch (code) {
+    case QVIT_OK: return "ok";
+    case QVIT_EINVAL: return "invalid argument (size, stride or enum)";
+    case QVIT_EALIGN: return "pointer or leading dimension not aligned as required";
+    case QVIT_ENULL: return "required pointer is NULL";
+    default: break;
+  }
+  if (code <= QVIT_EHIP) return hipGetErrorString((hipError_t)(QVIT_EHIP - code));
+  return "unknown qvit status";
+}
+
+const char* qvit_version(void) { return "qvit_hip 0.1 gfx950"; }
+
+static bool qtype_ok(int qtype) {
+  const int q = qtype & 0xff;
+  return (qtype & ~(0xff | QVIT_QT_FORCE_CAREFUL)) == 0 &&
+         (q == QVIT_QT_LINEAR || q == QVIT_QT_NONLINEAR || q == QVIT_QT_ULTRA_ACT);
+}
+
+static bool qptrs_ok(int qtype, const float* d, const float* qm, int levels) {
+  if ((qtype & 0xff) == QVIT_QT_ULTRA_ACT) return levels >= 1 && levels <= 127;
+  return d != nullptr && qm != nullptr;
+}
+
+int qvit_quantize_act_i8(const float* x, int64_t rows, int64_t cols, int64_t ldx, int qtype,
+                         const float* d_quant, const float* q_m, const float* t_quant, int levels,
+                         int8_t* codes, int64_t ldc, int64_t kpad, hipStream_t stream) {
+  if (!x || !codes) return QVIT_ENULL;
+  if (!qtype_ok(qtype) || !qptrs_ok(qtype, d_quant, q_m, levels)) return QVIT_EINVAL;
+  if (rows < 0 || cols < 0 || ldx < cols || kpad < cols || kpad % 16 || ldc < kpad) return QVIT_EINVAL;
+  if ((ldc % 16) || (((uintptr_t)codes) & 15)) return QVIT_EALIGN;
+  if (rows == 0 || kpad == 0) return QVIT_OK;
+  const int64_t work = rows * (kpad / 16);
+  hipLaunchKernelGGL(quantize_act_kernel, dim3(grid_for(work, kThreads)), dim3(kThreads), 0, stream,
+                     x, rows, cols, ldx, qtype, d_quant, q_m, t_quant, levels, codes, ldc, kpad);
+  return qvit_hip_status(hipGetLastError());
+}
+
+int qvit_fake_quant_f32(const float* x, int64_t n, int qtype, const float* d_quant,
+                        const float* q_m, const float* t_quant, int levels, float* y,
+                        hipStream_t stream) {
+  if (!x || !y) return QVIT_ENULL;
+  if (!qtype_ok(qtype) || !qptrs_ok(qtype, d_quant, q_m, levels)) return QVIT_EINVAL;
+  if (n < 0) return QVIT_EINVAL;
+  if (n == 0) return QVIT_OK;
+  hipLaunchKernelGGL(fake_quant_kernel, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, stream, x,
+                     n, qtype, d_quant, q_m, t_quant, levels, y);
+  return qvit_hip_status(hipGetLastError());
+}
+
+int qvit_pack_weight(const float* w, int64_t n, int64_t k, int64_t ldw, int qtype,
+                     const float* d_quant, const float* q_m, const float* t_quant, int wfmt,
+                     void* packed, int64_t npad, int64_t kpad, int32_t* overflow,
+                     hipStream_t stream) {
+  if (!w || !packed) return QVIT_ENULL;
+  const int q = qtype & 0xff;
+  if (!qtype_ok(qtype) || q == QVIT_QT_ULTRA_ACT || !d_quant || !q_m) return QVIT_EINVAL;
+  if (wfmt != QVIT_W4 && wfmt != QVIT_W8) return QVIT_EINVAL;
+  if (n <= 0 || k <= 0 || ldw < k || npad < n || kpad < k) return QVIT_EINVAL;
+  if (npad % QVIT_TILE_N || kpad % QVIT_TILE_K) return QVIT_EINVAL;
+  if (((uintptr_t)packed) & 15) return QVIT_EALIGN;
+  const int64_t work = npad * (kpad / 8);
+  if (wfmt == QVIT_W4) {
+    hipLaunchKernelGGL(pack_weight_kernel<QVIT_W4>, dim3(grid_for(work, kThreads)), dim3(kThreads),
+                       0, stream, w, n, k, ldw, qtype, d_quant, q_m, t_quant, packed, npad, kpad,
+                       overflow);
+  } else {
+    hipLaunchKernelGGL(pack_weight_kernel<QVIT_W8>, dim3(grid_for(work, kThreads)), dim3(kThreads),
+                       0, stream, w, n, k, ldw, qtype, d_quant, q_m, t_quant, packed, npad, kpad,
+                       overflow);
+  }
+  return qvit_hip_status(hipGetLastError());
+}
+
+int qvit_pad_bias(const float* bias, int64_t n, float* out, int64_t npad, hipStream_t stream) {
+  if (!out) return QVIT_ENULL;
+  if (n < 0 || npad < n) return QVIT_EINVAL;
+  if (npad == 0) return QVIT_OK;
+  hipLaunchKernelGGL(pad_bias_kernel, dim3(grid_for(npad, kThreads)), dim3(kThreads), 0, stream,
+                     bias, n, out, npad);
+  return qvit_hip_status(hipGetLastError());
+}
+
+int qvit_im2col_quant_i8(const float* x, int64_t B, int64_t C, int64_t H, int64_t W, int kh,
+                         int kw, int sh, int sw, int ph, int pw, int dh, int dw, int qtype,
+                         const float* d_quant, const float* q_m, const float* t_quant, int levels,
+                         int8_t* codes, int64_t ldc, int64_t kpad, hipStream_t stream) {
+  if (!x || !codes) return QVIT_ENULL;
+  if (!qtype_ok(qtype) || !qptrs_ok(qtype, d_quant, q_m, levels)) return QVIT_EINVAL;
+  if (B < 0 || C <= 0 || H <= 0 || W <= 0 || kh <= 0 || kw <= 0 || sh <= 0 || sw <= 0 || ph < 0 ||
+      pw < 0 || dh <= 0 || dw <= 0)
+    return QVIT_EINVAL;
+  const int64_t OH = (H + 2 * ph - (int64_t)dh * (kh - 1) - 1) / sh + 1;
+  const int64_t OW = (W + 2 * pw - (int64_t)dw * (kw - 1) - 1) / sw + 1;
+  const int64_t K = C * kh * kw;
+  if (OH <= 0 || OW <= 0 || kpad < K || kpad % 16 || ldc < kpad) return QVIT_EINVAL;
+  if ((ldc % 16) || (((uintptr_t)codes) & 15)) return QVIT_EALIGN;
+  if (B == 0) return QVIT_OK;
+  const int64_t work = B * OH * OW * (kpad / 16);
+  hipLaunchKernelGGL(im2col_quant_kernel, dim3(grid_for(work, kThreads)), dim3(kThreads), 0, stream,
+                     x, B, C, H, W, kh, kw, sh, sw, ph, pw, dh, dw, OH, OW, qtype, d_quant, q_m,
+                     t_quant, levels, codes, ldc, kpad);
+  return qvit_hip_status(hipGetLastError());
+}
+
+int qvit_layernorm_quant_i8(const float* x, int64_t rows, int64_t cols, int64_t ldx,
+                            const float* gamma, const float* beta, float eps, int qtype,
+                            const float* d_quant, const float* q_m, const float* t_quant,
+                            int levels, int8_t* codes, int64_t ldc, int64_t kpad,
+                            hipStream_t stream) {
+  if (!x || !codes) return QVIT_ENULL;
+  if (!qtype_ok(qtype) || !qptrs_ok(qtype, d_quant, q_m, levels)) return QVIT_EINVAL;
+  if (rows < 0 || cols <= 0 || ldx < cols || kpad < cols || ldc < kpad) return QVIT_EINVAL;
+  if (((ldc & 3) != 0) || (((uintptr_t)codes) & 3)) return QVIT_EALIGN;
+  if (rows == 0) return QVIT_OK;
+  const int64_t work = rows * 64;
+  hipLaunchKernelGGL(layernorm_quant_kernel, dim3(grid_for(work, kThreads)), dim3(kThreads), 0,
+                     stream, x, rows, cols, ldx, gamma, beta, eps, qtype, d_quant, q_m, t_quant,
+                     levels, codes, ldc, kpad);
+  return qvit_hip_status(hipGetLastError());
+}
+
+}  // extern "C"

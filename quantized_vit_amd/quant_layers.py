@@ -1,0 +1,443 @@
+"""QuantizeLinear / QuantizeConv2d for MI355X: the reference's module surface, HIP underneath.
+
+Mirrors OTO/quantization/quant_layers.py (OTO = QViT_with_GETA/only_train_once): same class
+names, constructor arguments, parameter names / state_dict keys (weight, bias, d_quant_wt, q_m_wt,
+[t_quant_wt], [d_quant_act, q_m_act, t_quant_act]), enums, from_module(), weight_bit /
+activation_bit and LAYER_TO_QUANTLAYER, so model_to_quantize_model and existing callers
+(vit_model.py:100,133,151,172,175,327) work unchanged.
+
+What differs is how forward() computes (quant_layers.py:495-499, 575-587). The reference
+re-quantizes the fp32 master weight on every call and runs an fp32 F.linear on fake-quant
+operands. Here, on a ROCm device:
+  * weights are quantized once per parameter version into int4 (|level| <= 7) or int8 codes,
+    packed for the MFMA kernel (qvit_pack_weight), and cached;
+  * activations are quantized to int8 codes by a HIP kernel (qvit_quantize_act_i8);
+  * the product is an exact int32 MFMA contraction with the fp32 epilogue
+    d_act * d_wt * acc + bias (qvit_gemm) — mathematically the reference's F.linear on
+    d_a*k_a and d_w*k_w, differing only in fp32 rounding.
+Layers whose levels do not fit int8 (e.g. the 16/32-bit initial states, weight-only mode) run
+the reference's fake-quant values (HIP kernel qvit_fake_quant_f32) through the library fp32
+GEMM instead. CPU tensors are rejected: the product has no CPU fallback.
+
+Inference only: the HIP path does not record autograd history (training / GETA is out of scope).
+"""
+from __future__ import annotations
+
+import logging
+import math
+import warnings
+from dataclasses import dataclass, field
+from enum import Enum
+from typing import Optional, Tuple, Union
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+
+logger = logging.getLogger(__name__)
+
+
+class NanInGradientError(Exception):
+    """quant_layers.py:10-13 (raised by the reference's backward; kept for API parity)."""
+
+    def __init__(self, message):
+        self.message = message
+        super().__init__(self.message)
+
+
+class QuantizationType(Enum):
+    """quant_layers.py:20-24."""
+    SYMMETRIC_LINEAR = "symmetric+linear"
+    SYMMETRIC_NONLINEAR = "symmetric+nonlinear"
+    DGE = "dge"
+
+
+class QuantizationMode(Enum):
+    """quant_layers.py:27-29."""
+    WEIGHT_ONLY = "weight_only"
+    WEIGHT_AND_ACTIVATION = "weight_and_activation"
+
+
+def _qtype_code(qt: QuantizationType) -> int:
+    # DGEQuantizer.forward (quant_layers.py:217-246) is the linear quantizer's forward
+    if qt in (QuantizationType.SYMMETRIC_LINEAR, QuantizationType.DGE):
+        return _lib.QT_LINEAR
+    if qt == QuantizationType.SYMMETRIC_NONLINEAR:
+        return _lib.QT_NONLINEAR
+    raise NotImplementedError(qt)
+
+
+_warned_grad = False
+
+
+def _warn_no_grad() -> None:
+    global _warned_grad
+    if not _warned_grad:
+        _warned_grad = True
+        warnings.warn("quantized_vit_amd: the HIP forward path records no autograd history "
+                      "(inference only); run under torch.no_grad() to silence this warning.")
+
+
+def _as_param_ptr(p: Optional[torch.Tensor], device: torch.device) -> Optional[torch.Tensor]:
+    if p is None:
+        return None
+    t = p.detach()
+    if t.device != device or t.dtype != torch.float32 or not t.is_contiguous():
+        t = t.to(device=device, dtype=torch.float32).contiguous()
+    return t
+
+
+def saturation_level(qtype: int, d: float, q_m: float, t: float = 1.0) -> float:
+    """Host copy of the device formula: rne(|q_m| / d) (linear, quant_layers.py:154,159) or
+    rne(exp(t log(|q_m| + 1e-6)) / d) (nonlinear, :62,67), in fp32."""
+    f = np.float32
+    with np.errstate(all="ignore"):
+        if qtype == _lib.QT_LINEAR:
+            p = np.abs(f(q_m))
+        else:
+            p = np.exp(f(t) * np.log(np.abs(f(q_m)) + f(1e-6)), dtype=np.float32)
+        q = f(p) / f(d)
+    return float(np.rint(q)) if np.isfinite(q) else float("inf")
+
+
+def _round_up(v: int, m: int) -> int:
+    return (v + m - 1) // m * m
+
+
+@dataclass
+class QuantPlan:
+    """Per-layer device state derived from the parameters (rebuilt when any of them changes)."""
+    key: tuple
+    device: torch.device
+    qtype: int
+    n: int
+    k: int
+    npad: int
+    kpad: int
+    wfmt: int                       # _lib.W4 / _lib.W8 / 0 (fp32 fake-quant path)
+    int_path: bool                  # activation codes fit int8 and the weight was packed
+    level_wt: float
+    level_act: float
+    packed: Optional[torch.Tensor] = None
+    bias_pad: Optional[torch.Tensor] = None
+    w_fakequant: Optional[torch.Tensor] = None
+    d_wt: Optional[torch.Tensor] = None
+    qm_wt: Optional[torch.Tensor] = None
+    t_wt: Optional[torch.Tensor] = None
+    d_act: Optional[torch.Tensor] = None
+    qm_act: Optional[torch.Tensor] = None
+    t_act: Optional[torch.Tensor] = None
+    extra: dict = field(default_factory=dict)
+
+
+class QuantizeMixin:
+    """quant_layers.py:303-410 — parameters, quantize_weight/quantize_act, bit-width properties."""
+
+    def init_quantization(
+        self,
+        d_quant_init: float = 1.0,
+        t_quant_init: float = 1.0,
+        q_m_init: float = 1.0,
+        quant_type: QuantizationType = QuantizationType.SYMMETRIC_LINEAR,
+        quant_mode: QuantizationMode = QuantizationMode.WEIGHT_ONLY,
+        weight_clip_val: Tuple[float, float] = (-2.0, 2.0),
+        act_clip_val: Tuple[float, float] = (-2.0, 2.0),
+    ):
+        self.d_quant_wt = nn.Parameter(torch.tensor([d_quant_init]))
+        self.q_m_wt = nn.Parameter(torch.tensor([q_m_init]))
+        if quant_type == QuantizationType.SYMMETRIC_NONLINEAR:
+            self.t_quant_wt = nn.Parameter(torch.tensor([t_quant_init]))
+        if quant_mode == QuantizationMode.WEIGHT_AND_ACTIVATION:
+            self.d_quant_act = nn.Parameter(torch.tensor([d_quant_init]))
+            self.q_m_act = nn.Parameter(torch.tensor([q_m_init]))
+            if quant_type == QuantizationType.SYMMETRIC_NONLINEAR:
+                self.t_quant_act = nn.Parameter(torch.tensor([t_quant_init]))
+        self.quant_type = quant_type
+        self.quant_mode = quant_mode
+        self.weight_clip_val = weight_clip_val
+        self.act_clip_val = act_clip_val
+        self._qplan: Optional[QuantPlan] = None
+
+    # -- reference API: fake-quant fp32 tensors (quant_layers.py:332-381) -------------------
+    def quantize_weight(self, weight: torch.Tensor) -> torch.Tensor:
+        dev = weight.device
+        return _lib.fake_quant_f32(weight.detach(), _qtype_code(self.quant_type),
+                                   _as_param_ptr(self.d_quant_wt, dev), _as_param_ptr(self.q_m_wt, dev),
+                                   _as_param_ptr(getattr(self, "t_quant_wt", None), dev))
+
+    def quantize_act(self, activation: torch.Tensor) -> torch.Tensor:
+        if self.quant_mode != QuantizationMode.WEIGHT_AND_ACTIVATION:
+            return activation
+        dev = activation.device
+        return _lib.fake_quant_f32(activation.detach(), _qtype_code(self.quant_type),
+                                   _as_param_ptr(self.d_quant_act, dev), _as_param_ptr(self.q_m_act, dev),
+                                   _as_param_ptr(getattr(self, "t_quant_act", None), dev))
+
+    @property
+    def weight_bit(self) -> int:
+        d = self.d_quant_wt.item()
+        qmax = abs(self.q_m_wt.item())
+        if self.quant_type == QuantizationType.SYMMETRIC_LINEAR:
+            t = 1.0
+        elif self.quant_type == QuantizationType.SYMMETRIC_NONLINEAR:
+            t = self.t_quant_wt.item()
+        else:
+            raise NotImplementedError
+        return round(math.log2(math.exp(t * math.log(qmax)) / abs(d) + 1) + 1)
+
+    @property
+    def activation_bit(self) -> int:
+        if self.quant_mode != QuantizationMode.WEIGHT_AND_ACTIVATION:
+            return 32
+        d = self.d_quant_act.item()
+        qmax = abs(self.q_m_act.item())
+        if self.quant_type == QuantizationType.SYMMETRIC_LINEAR:
+            t = 1.0
+        elif self.quant_type == QuantizationType.SYMMETRIC_NONLINEAR:
+            t = self.t_quant_act.item()
+        else:
+            raise NotImplementedError
+        return round(math.log2(math.exp(t * math.log(qmax)) / abs(d) + 1) + 1)
+
+    # -- MI355X state ---------------------------------------------------------------------------
+    def invalidate(self) -> None:
+        """Drops the cached quantized weight. Needed only after editing parameters through
+        `.data` (which bypasses the version counter the cache keys on)."""
+        self._qplan = None
+
+    def _quant_param_tensors(self):
+        names = ["weight", "bias", "d_quant_wt", "q_m_wt", "t_quant_wt", "d_quant_act", "q_m_act", "t_quant_act"]
+        return [getattr(self, n, None) for n in names]
+
+    def _plan_key(self) -> tuple:
+        key = [self.quant_type, self.quant_mode, self.training]
+        for p in self._quant_param_tensors():
+            key.append(None if p is None else (p.data_ptr(), p._version, p.device, p.dtype, tuple(p.shape)))
+        return tuple(key)
+
+    def _weight_2d(self) -> torch.Tensor:
+        w = self.weight.detach()
+        return w.reshape(w.shape[0], -1)
+
+    def quant_plan(self) -> QuantPlan:
+        """Builds (or returns the cached) device plan. Building syncs the host once (it reads the
+        scalar quantizer parameters to choose int4 / int8 / fp32 storage)."""
+        key = self._plan_key()
+        plan = self._qplan
+        if plan is not None and plan.key == key and not self.training:
+            return plan
+        plan = self._build_plan(key)
+        self._qplan = plan
+        return plan
+
+    def _build_plan(self, key: tuple) -> QuantPlan:
+        w2 = self._weight_2d()
+        dev = w2.device
+        if not w2.is_cuda:
+            raise _lib.QvitError(f"{type(self).__name__}: weights are on {dev}; move the model to a ROCm "
+                                 "device (the HIP path has no CPU fallback)")
+        qt = _qtype_code(self.quant_type)
+        n, k = w2.shape
+        npad, kpad = _round_up(n, _lib.TILE_N), _round_up(k, _lib.TILE_K)
+        d_wt = _as_param_ptr(self.d_quant_wt, dev)
+        qm_wt = _as_param_ptr(self.q_m_wt, dev)
+        t_wt = _as_param_ptr(getattr(self, "t_quant_wt", None), dev)
+        wa = self.quant_mode == QuantizationMode.WEIGHT_AND_ACTIVATION
+        d_act = _as_param_ptr(getattr(self, "d_quant_act", None), dev) if wa else None
+        qm_act = _as_param_ptr(getattr(self, "q_m_act", None), dev) if wa else None
+        t_act = _as_param_ptr(getattr(self, "t_quant_act", None), dev) if wa else None
+        # one host sync: the scalar parameters decide the storage format
+        scal = torch.stack([x.reshape(-1)[0] for x in (d_wt, qm_wt, t_wt if t_wt is not None else d_wt)]
+                           + ([d_act.reshape(-1)[0], qm_act.reshape(-1)[0],
+                               (t_act if t_act is not None else d_act).reshape(-1)[0]] if wa else [])).cpu()
+        s = scal.tolist()
+        lw = saturation_level(qt, s[0], s[1], s[2] if t_wt is not None else 1.0)
+        la = saturation_level(qt, s[3], s[4], s[5] if t_act is not None else 1.0) if wa else float("inf")
+        plan = QuantPlan(key=key, device=dev, qtype=qt, n=n, k=k, npad=npad, kpad=kpad, wfmt=0, int_path=False,
+                         level_wt=lw, level_act=la, d_wt=d_wt, qm_wt=qm_wt, t_wt=t_wt, d_act=d_act,
+                         qm_act=qm_act, t_act=t_act)
+        w32 = w2 if (w2.dtype == torch.float32 and w2.is_contiguous()) else w2.float().contiguous()
+        act_ok = wa and abs(la) <= 127
+        if act_ok and abs(lw) <= 127:
+            overflow = torch.zeros(1, dtype=torch.int32, device=dev)
+            for wfmt in ((_lib.W4, _lib.W8) if abs(lw) <= 7 else (_lib.W8,)):
+                overflow.zero_()
+                packed = _lib.pack_weight(w32, qt, d_wt, qm_wt, t_wt, wfmt, npad, kpad, overflow)
+                if int(overflow.item()) == 0:
+                    plan.packed, plan.wfmt, plan.int_path = packed, wfmt, True
+                    break
+        if plan.int_path:
+            bias = self.bias.detach() if self.bias is not None else None
+            plan.bias_pad = _lib.pad_bias(bias, n, npad, dev)
+        else:
+            wq = _lib.fake_quant_f32(self.weight.detach().float(), qt, d_wt, qm_wt, t_wt)
+            plan.w_fakequant = wq
+        return plan
+
+    def _check_input(self, x: torch.Tensor) -> None:
+        if not x.is_cuda:
+            raise _lib.QvitError(f"{type(self).__name__}: input on {x.device}; the HIP path needs a ROCm "
+                                 "device tensor (no CPU fallback)")
+        if torch.is_grad_enabled() and (x.requires_grad or any(
+                p is not None and p.requires_grad for p in self._quant_param_tensors())):
+            _warn_no_grad()
+
+    def _act_codes(self, x2d: torch.Tensor, plan: QuantPlan) -> torch.Tensor:
+        M = x2d.shape[0]
+        codes = torch.empty((M, plan.kpad), dtype=torch.int8, device=x2d.device)
+        _lib.quantize_act_i8(x2d, plan.qtype, plan.d_act, plan.qm_act, plan.t_act, 0, codes, plan.kpad)
+        return codes
+
+    def gemm_codes(self, codes: torch.Tensor, plan: QuantPlan, epilogue: int = _lib.EPI_F32,
+                   out: Optional[torch.Tensor] = None, next_layer: Optional["QuantizeMixin"] = None) -> torch.Tensor:
+        """Runs the contraction on activation codes (int8 [M, kpad]) with the given epilogue.
+        EPI_I8 / EPI_I8_GELU quantize the result with `next_layer`'s activation quantizer."""
+        M = codes.shape[0]
+        dev = codes.device
+        oq = dict(out_qtype=0)
+        if epilogue in (_lib.EPI_I8, _lib.EPI_I8_GELU):
+            nplan = next_layer.quant_plan()
+            if out is None:
+                out = torch.empty((M, _round_up(plan.n, 16)), dtype=torch.int8, device=dev)
+            oq = dict(out_qtype=nplan.qtype, out_d=nplan.d_act, out_qm=nplan.qm_act, out_t=nplan.t_act)
+        elif epilogue == _lib.EPI_I32:
+            if out is None:
+                out = torch.empty((M, _round_up(plan.n, 4)), dtype=torch.int32, device=dev)
+        elif out is None:
+            out = torch.empty((M, _round_up(plan.n, 4)), dtype=torch.float32, device=dev)
+        _lib.gemm(codes, M, plan.kpad, plan.packed, plan.wfmt, plan.n, plan.npad, plan.d_act, plan.d_wt,
+                  plan.bias_pad, epilogue, out, **oq)
+        return out
+
+
+def initialize_quant_layer(layer, num_bits: int = 16,
+                           quant_type: QuantizationType = QuantizationType.SYMMETRIC_LINEAR,
+                           quant_mode: QuantizationMode = QuantizationMode.WEIGHT_ONLY) -> None:
+    """quant_layers.py:413-440: q_m = max|W|, d = q_m / (2^(b-1) - 1), t = 1; the activation
+    parameters start from the same weight statistics (:436-438)."""
+    if not isinstance(layer, (QuantizeConv2d, QuantizeLinear)):
+        return
+    num_bits = float(num_bits)
+    t_quant_init = 1.0
+    q_s = torch.tensor(0.0, device=layer.weight.device)
+    qm_quant_init = torch.max(torch.abs(layer.weight))
+    d_quant_init = (qm_quant_init - q_s) / (2 ** (num_bits - 1) - 1)
+    nn.init.constant_(layer.d_quant_wt, d_quant_init)
+    nn.init.constant_(layer.q_m_wt, qm_quant_init)
+    if quant_type == QuantizationType.SYMMETRIC_NONLINEAR:
+        nn.init.constant_(layer.t_quant_wt, t_quant_init)
+    if quant_mode == QuantizationMode.WEIGHT_AND_ACTIVATION:
+        nn.init.constant_(layer.d_quant_act, d_quant_init)
+        nn.init.constant_(layer.q_m_act, qm_quant_init)
+        if quant_type == QuantizationType.SYMMETRIC_NONLINEAR:
+            nn.init.constant_(layer.t_quant_act, t_quant_init)
+    layer.invalidate()
+
+
+class QuantizeLinear(nn.Linear, QuantizeMixin):
+    """quant_layers.py:443-499."""
+
+    def __init__(self, in_features, out_features, bias=True, d_quant_init=1.0, t_quant_init=1.0, q_m_init=1.0,
+                 quant_type=QuantizationType.SYMMETRIC_LINEAR, quant_mode=QuantizationMode.WEIGHT_ONLY):
+        nn.Linear.__init__(self, in_features, out_features, bias)
+        self.init_quantization(d_quant_init, t_quant_init, q_m_init, quant_type, quant_mode)
+
+    @staticmethod
+    def from_module(module=None, d_quant_init=1.0, t_quant_init=1.0, q_m_init=1.0,
+                    quant_type=QuantizationType.SYMMETRIC_LINEAR, quant_mode=QuantizationMode.WEIGHT_ONLY,
+                    quant_init_by_module=True, num_bits=8):
+        q = QuantizeLinear(in_features=module.in_features, out_features=module.out_features,
+                           bias=module.bias is not None, d_quant_init=d_quant_init, t_quant_init=t_quant_init,
+                           q_m_init=q_m_init, quant_type=quant_type, quant_mode=quant_mode)
+        q = q.to(device=module.weight.device)
+        q.weight.data.copy_(module.weight.data)
+        if module.bias is not None:
+            q.bias.data.copy_(module.bias.data)
+        if quant_init_by_module:
+            initialize_quant_layer(q, num_bits=num_bits, quant_type=quant_type, quant_mode=quant_mode)
+        return q
+
+    def forward(self, input_: torch.Tensor) -> torch.Tensor:
+        self._check_input(input_)
+        plan = self.quant_plan()
+        if plan.int_path:
+            x2 = input_.detach().reshape(-1, plan.k)
+            if x2.dtype != torch.float32 or x2.stride(-1) != 1:
+                x2 = x2.float().contiguous()
+            codes = self._act_codes(x2, plan)
+            out = self.gemm_codes(codes, plan, _lib.EPI_F32)
+            if out.shape[1] != plan.n:
+                out = out[:, :plan.n].contiguous()
+            return out.view(*input_.shape[:-1], plan.n)
+        x = self.quantize_act(input_.float()) if self.quant_mode == QuantizationMode.WEIGHT_AND_ACTIVATION \
+            else input_.float()
+        return F.linear(x.detach(), plan.w_fakequant, None if self.bias is None else self.bias.detach())
+
+
+class QuantizeConv2d(nn.Conv2d, QuantizeMixin):
+    """quant_layers.py:502-587."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=1, dilation=1, groups=1,
+                 bias=False, d_quant_init=1.0, t_quant_init=1.0, q_m_init=1.0,
+                 quant_type=QuantizationType.SYMMETRIC_LINEAR, quant_mode=QuantizationMode.WEIGHT_ONLY):
+        nn.Conv2d.__init__(self, in_channels, out_channels, kernel_size, stride, padding, dilation, groups,
+                           bias=bias)
+        self.init_quantization(d_quant_init, t_quant_init, q_m_init, quant_type, quant_mode)
+
+    @staticmethod
+    def from_module(module=None, d_quant_init=1.0, t_quant_init=1.0, q_m_init=1.0,
+                    quant_type=QuantizationType.SYMMETRIC_LINEAR, quant_mode=QuantizationMode.WEIGHT_ONLY,
+                    quant_init_by_module=True, num_bits=8):
+        q = QuantizeConv2d(in_channels=module.in_channels, out_channels=module.out_channels,
+                           kernel_size=module.kernel_size, stride=module.stride, padding=module.padding,
+                           dilation=module.dilation, groups=module.groups, bias=module.bias is not None,
+                           d_quant_init=d_quant_init, t_quant_init=t_quant_init, q_m_init=q_m_init,
+                           quant_type=quant_type, quant_mode=quant_mode)
+        q = q.to(device=module.weight.device)
+        q.weight.data.copy_(module.weight.data)
+        if module.bias is not None:
+            q.bias.data.copy_(module.bias.data)
+        if quant_init_by_module:
+            initialize_quant_layer(q, num_bits=num_bits, quant_type=quant_type, quant_mode=quant_mode)
+        return q
+
+    def _int_conv_ok(self) -> bool:
+        return (self.groups == 1 and self.padding_mode == "zeros" and not isinstance(self.padding, str))
+
+    def conv_codes_gemm(self, input_: torch.Tensor, epilogue: int = _lib.EPI_F32):
+        """im2col + quantize + contraction. Returns ([B*OH*OW, Cout] NHWC rows, (B, OH, OW))."""
+        plan = self.quant_plan()
+        x = input_.detach()
+        if x.dtype != torch.float32 or not x.is_contiguous():
+            x = x.float().contiguous()
+        B, C, H, W = x.shape
+        kh, kw = self.kernel_size
+        sh, sw = self.stride
+        ph, pw = self.padding
+        dh, dw = self.dilation
+        OH = (H + 2 * ph - dh * (kh - 1) - 1) // sh + 1
+        OW = (W + 2 * pw - dw * (kw - 1) - 1) // sw + 1
+        codes = torch.empty((B * OH * OW, plan.kpad), dtype=torch.int8, device=x.device)
+        _lib.im2col_quant_i8(x, kh, kw, sh, sw, ph, pw, dh, dw, plan.qtype, plan.d_act, plan.qm_act, plan.t_act, 0,
+                             codes, plan.kpad)
+        out = self.gemm_codes(codes, plan, epilogue)
+        return out, (B, OH, OW)
+
+    def forward(self, input_: torch.Tensor) -> torch.Tensor:
+        self._check_input(input_)
+        plan = self.quant_plan()
+        if plan.int_path and self._int_conv_ok():
+            out, (B, OH, OW) = self.conv_codes_gemm(input_)
+            n = plan.n
+            return out[:, :n].reshape(B, OH, OW, n).permute(0, 3, 1, 2).contiguous()
+        x = self.quantize_act(input_.float()) if self.quant_mode == QuantizationMode.WEIGHT_AND_ACTIVATION \
+            else input_.float()
+        w = plan.w_fakequant.view_as(self.weight)
+        return F.conv2d(x.detach(), w, None if self.bias is None else self.bias.detach(), self.stride,
+                        self.padding, self.dilation, self.groups)
+
+
+LAYER_TO_QUANTLAYER = {"Linear": QuantizeLinear, "Conv2d": QuantizeConv2d}

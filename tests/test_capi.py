@@ -1,0 +1,78 @@
+"""The C-ABI library loads and exports exactly what include/qvit_hip.h declares; argument validation
+follows the header's status conventions. No kernel is launched (runs without a GPU)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from quantized_vit_amd import _lib, build
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "qvit_hip.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(qvit_\w+)\s*\(", text)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    build.build()
+    return _lib.load()
+
+
+def test_header_matches_binding():
+    assert declared_functions() == _lib.EXPORTED_SYMBOLS
+
+
+def test_library_exports_every_declared_symbol(lib):
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+
+
+def test_version_and_strerror(lib):
+    assert "gfx950" in _lib.version()
+    assert lib.qvit_strerror(0) == b"ok"
+    assert b"invalid" in lib.qvit_strerror(-1)
+    assert b"NULL" in lib.qvit_strerror(-3)
+
+
+def test_constants_match_header():
+    text = open(HEADER).read()
+    consts = dict(re.findall(r"#define\s+(QVIT_\w+)\s+(-?\d+)", text))
+    assert int(consts["QVIT_QT_LINEAR"]) == _lib.QT_LINEAR
+    assert int(consts["QVIT_QT_NONLINEAR"]) == _lib.QT_NONLINEAR
+    assert int(consts["QVIT_QT_ULTRA_ACT"]) == _lib.QT_ULTRA_ACT
+    assert int(consts["QVIT_W4"]) == _lib.W4 and int(consts["QVIT_W8"]) == _lib.W8
+    for e in ("F32", "F32_RESID", "I8_GELU", "I8", "I32"):
+        assert int(consts[f"QVIT_EPI_{e}"]) == getattr(_lib, f"EPI_{e}")
+    assert int(consts["QVIT_TILE_N"]) == _lib.TILE_N and int(consts["QVIT_TILE_K"]) == _lib.TILE_K
+
+
+def test_argument_validation_without_launch(lib):
+    fake = ctypes.c_void_p(0x1000)   # never dereferenced: validation rejects before any launch
+    # NULL operands
+    assert lib.qvit_gemm(None, 16, 128, 128, fake, 4, 16, 128, fake, fake, None, 0, fake, 16, 0, None, None,
+                         None, 0, None) == -3
+    # K not a multiple of the tile
+    assert lib.qvit_gemm(fake, 16, 100, 128, fake, 4, 16, 128, fake, fake, None, 0, fake, 16, 0, None, None,
+                         None, 0, None) == -1
+    # bad weight format
+    assert lib.qvit_gemm(fake, 16, 128, 128, fake, 5, 16, 128, fake, fake, None, 0, fake, 16, 0, None, None,
+                         None, 0, None) == -1
+    # misaligned activation stride
+    assert lib.qvit_gemm(fake, 16, 128, 136, fake, 4, 16, 128, fake, fake, None, 0, fake, 16, 0, None, None,
+                         None, 0, None) == -2
+    # bad quantizer enum
+    assert lib.qvit_quantize_act_i8(fake, 4, 16, 16, 7, fake, fake, None, 0, fake, 16, 16, None) == -1
+    # kpad not a multiple of 16
+    assert lib.qvit_quantize_act_i8(fake, 4, 10, 16, 0, fake, fake, None, 0, fake, 16, 12, None) == -1
+    # ULTRA activation quantizer needs a level count in [1, 127]
+    assert lib.qvit_quantize_act_i8(fake, 4, 16, 16, 2, None, None, None, 0, fake, 16, 16, None) == -1
+    # weight packing: npad must be a multiple of the tile
+    assert lib.qvit_pack_weight(fake, 10, 128, 128, 0, fake, fake, None, 4, fake, 100, 128, None, None) == -1
+    # zero-size work is a no-op success
+    assert lib.qvit_quantize_act_i8(fake, 0, 16, 16, 0, fake, fake, None, 0, fake, 16, 16, None) == 0

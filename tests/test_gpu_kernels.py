@@ -1,0 +1,233 @@
+"""GPU parity of the HIP kernels (through the C-ABI) against the CPU oracle.
+
+Bars:
+  * integer work (packing, MFMA accumulation, linear-quantizer codes): bit-exact;
+  * nonlinear-quantizer codes (exp/log in fp32: ocml on the GPU vs the CPU's libm/Sleef): identical
+    except at ulp-level rounding-boundary ties, bounded here at <= 1e-4 of elements, each off by 1;
+  * fp32 epilogues: relative error <= 1e-6 against fp64 evaluation of the same integer result.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import quant_oracle as O
+from quantized_vit_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+QT = {O.LINEAR: _lib.QT_LINEAR, O.NONLINEAR: _lib.QT_NONLINEAR}
+
+
+def _p(v, dev):
+    return torch.tensor([float(v)], dtype=torch.float32, device=dev)
+
+
+def _round_up(v, m):
+    return (v + m - 1) // m * m
+
+
+def pack_codes(codes_w: torch.Tensor, wfmt: int, dev):
+    """Packs integer weight codes exactly (linear quantizer with d = 1, q_m large => code = w)."""
+    n, k = codes_w.shape
+    npad, kpad = _round_up(n, 128), _round_up(k, 128)
+    w = codes_w.float().to(dev).contiguous()
+    ovf = torch.zeros(1, dtype=torch.int32, device=dev)
+    packed = _lib.pack_weight(w, _lib.QT_LINEAR, _p(1.0, dev), _p(1000.0, dev), None, wfmt, npad, kpad, ovf)
+    torch.cuda.synchronize()
+    assert ovf.item() == 0
+    return packed, npad, kpad
+
+
+def act_buffer(codes_a: torch.Tensor, kpad: int, dev):
+    m, k = codes_a.shape
+    A = torch.zeros((m, kpad), dtype=torch.int8, device=dev)
+    A[:, :k] = codes_a.to(torch.int8).to(dev)
+    return A
+
+
+SHAPES = [(1, 1, 1), (128, 128, 128), (300, 200, 200), (257, 2304, 768), (1576, 768, 192), (7, 15, 768),
+          (33, 3072, 768), (129, 768, 3072), (64, 100, 1000)]
+
+
+@pytest.mark.parametrize("wfmt", [_lib.W4, _lib.W8])
+@pytest.mark.parametrize("M,N,K", SHAPES)
+def test_gemm_int32_exact(dev, wfmt, M, N, K):
+    g = torch.Generator().manual_seed(M * 7 + N * 13 + K)
+    a = torch.randint(-127, 128, (M, K), generator=g)
+    lim = 8 if wfmt == _lib.W4 else 128
+    w = torch.randint(-lim, lim, (N, K), generator=g)
+    packed, npad, kpad = pack_codes(w, wfmt, dev)
+    A = act_buffer(a, kpad, dev)
+    C = torch.full((M, _round_up(N, 4)), -7, dtype=torch.int32, device=dev)
+    _lib.gemm(A, M, kpad, packed, wfmt, N, npad, None, None, None, _lib.EPI_I32, C)
+    torch.cuda.synchronize()
+    ref = O.int_accumulators(a.float(), w.float())
+    assert torch.equal(C[:, :N].cpu().long(), ref)
+    if C.shape[1] > N:
+        assert (C[:, N:] == -7).all()   # nothing written past N
+
+
+def test_gemm_extreme_values_exact(dev):
+    M, N, K = 130, 256, 4096
+    a = torch.full((M, K), -127)
+    w = torch.full((N, K), -8)
+    a[1::2] = 127
+    w[1::3] = 7
+    packed, npad, kpad = pack_codes(w, _lib.W4, dev)
+    C = torch.empty((M, N), dtype=torch.int32, device=dev)
+    _lib.gemm(act_buffer(a, kpad, dev), M, kpad, packed, _lib.W4, N, npad, None, None, None, _lib.EPI_I32, C)
+    assert torch.equal(C.cpu().long(), O.int_accumulators(a.float(), w.float()))
+
+
+@pytest.mark.parametrize("epi", [_lib.EPI_F32, _lib.EPI_F32_RESID])
+def test_gemm_f32_epilogues(dev, epi):
+    M, N, K = 515, 384, 768
+    g = torch.Generator().manual_seed(5)
+    a = torch.randint(-127, 128, (M, K), generator=g)
+    w = torch.randint(-7, 8, (N, K), generator=g)
+    bias = torch.randn(N, generator=g)
+    packed, npad, kpad = pack_codes(w, _lib.W4, dev)
+    d_a, d_w = 0.0123, 0.00457
+    bias_pad = _lib.pad_bias(bias.to(dev), N, npad, dev)
+    base = torch.randn(M, N, generator=g)
+    C = base.clone().to(dev) if epi == _lib.EPI_F32_RESID else torch.empty((M, N), device=dev)
+    _lib.gemm(act_buffer(a, kpad, dev), M, kpad, packed, _lib.W4, N, npad, _p(d_a, dev), _p(d_w, dev), bias_pad,
+              epi, C)
+    acc = O.int_accumulators(a.float(), w.float()).double()
+    alpha = float(np.float32(d_a) * np.float32(d_w))
+    ref = alpha * acc + bias.double()
+    if epi == _lib.EPI_F32_RESID:
+        ref = ref + base.double()
+    err = (C.cpu().double() - ref).abs().max() / ref.abs().max()
+    assert err < 1e-6, err
+
+
+@pytest.mark.parametrize("gelu", [False, True])
+@pytest.mark.parametrize("qt,t", [(O.LINEAR, 1.0), (O.NONLINEAR, 1.0), (O.NONLINEAR, 0.85)])
+def test_gemm_int8_code_epilogue(dev, gelu, qt, t):
+    M, N, K = 300, 640, 768
+    g = torch.Generator().manual_seed(11)
+    a = torch.randint(-127, 128, (M, K), generator=g)
+    w = torch.randint(-7, 8, (N, K), generator=g)
+    bias = torch.randn(N, generator=g) * 0.1
+    packed, npad, kpad = pack_codes(w, _lib.W4, dev)
+    d_a, d_w = 0.002, 0.0011
+    bias_pad = _lib.pad_bias(bias.to(dev), N, npad, dev)
+    dn, qmn = 0.9 / 127, 0.9
+    out = torch.empty((M, _round_up(N, 16)), dtype=torch.int8, device=dev)
+    _lib.gemm(act_buffer(a, kpad, dev), M, kpad, packed, _lib.W4, N, npad, _p(d_a, dev), _p(d_w, dev), bias_pad,
+              _lib.EPI_I8_GELU if gelu else _lib.EPI_I8, out, out_qtype=QT[qt], out_d=_p(dn, dev),
+              out_qm=_p(qmn, dev), out_t=_p(t, dev) if qt == O.NONLINEAR else None)
+    # reference: fp32 epilogue value, torch GELU (erf), oracle quantizer codes
+    acc = O.int_accumulators(a.float(), w.float()).float()
+    v = (torch.tensor(d_a, dtype=torch.float32) * torch.tensor(d_w, dtype=torch.float32)) * acc + bias
+    if gelu:
+        v = F.gelu(v)
+    ref = O.quant_codes(v, qt, dn, qmn, t)
+    got = out[:, :N].cpu().float()
+    diff = (got - ref).abs()
+    assert diff.max() <= 1
+    # the fp32 epilogue value itself differs by ulps (fma vs mul+add, erf implementation), so
+    # boundary ties may flip; require them to be rare
+    assert (diff > 0).float().mean() <= 2e-4
+
+
+def _quant_inputs(g, n=300_000, scale=0.6):
+    x = torch.randn(n, generator=g) * scale
+    x[:1000] = 0.0
+    x[1000:2000] = (torch.arange(-500, 500, dtype=torch.float32) + 0.5) * 0.01   # near/at ties
+    return x
+
+
+@pytest.mark.parametrize("qt,d,qm,t", [(O.LINEAR, 0.01, 1.0, 1.0), (O.LINEAR, 1 / 127, 1.0, 1.0),
+                                       (O.NONLINEAR, 0.01, 1.0, 1.0), (O.NONLINEAR, 0.02, 1.5, 0.9),
+                                       (O.NONLINEAR, 0.005, 0.8, 1.25), (O.LINEAR, 0.05, -0.5, 1.0)])
+def test_quantize_act_codes_vs_oracle(dev, qt, d, qm, t):
+    g = torch.Generator().manual_seed(3)
+    x = _quant_inputs(g)
+    rows, cols = 600, 500
+    x2 = x.view(rows, cols)
+    kpad = 512
+    tt = _p(t, dev) if qt == O.NONLINEAR else None
+    fast = torch.empty((rows, kpad), dtype=torch.int8, device=dev)
+    careful = torch.empty_like(fast)
+    _lib.quantize_act_i8(x2.to(dev), QT[qt], _p(d, dev), _p(qm, dev), tt, 0, fast, kpad)
+    _lib.quantize_act_i8(x2.to(dev), QT[qt] | _lib.QT_FORCE_CAREFUL, _p(d, dev), _p(qm, dev), tt, 0, careful, kpad)
+    fast, careful = fast.cpu(), careful.cpu()
+    assert torch.equal(fast, careful), "guarded fast path must equal the careful path bit for bit"
+    assert (fast[:, cols:] == 0).all()
+    ref = O.quant_codes(x2, qt, d, qm, t)
+    got = fast[:, :cols].float()
+    if qt == O.LINEAR:
+        assert torch.equal(got, ref)
+    else:
+        diff = (got - ref).abs()
+        assert diff.max() <= 1
+        assert (diff > 0).float().mean() <= 1e-4, (diff > 0).float().mean()
+
+
+@pytest.mark.parametrize("qt,t", [(O.LINEAR, 1.0), (O.NONLINEAR, 1.0), (O.NONLINEAR, 0.7)])
+def test_fake_quant_values_vs_oracle(dev, qt, t):
+    g = torch.Generator().manual_seed(4)
+    x = _quant_inputs(g, 100_000)
+    d, qm = 0.013, 1.1
+    y = _lib.fake_quant_f32(x.to(dev), QT[qt], _p(d, dev), _p(qm, dev), _p(t, dev) if qt == O.NONLINEAR else None)
+    ref = O.fake_quant(x, qt, d, qm, t)
+    if qt == O.LINEAR:
+        assert torch.equal(y.cpu(), ref)
+    else:
+        assert ((y.cpu() - ref).abs() > 0).float().mean() <= 1e-4
+
+
+def test_pack_weight_overflow_flag(dev):
+    w = torch.linspace(-1, 1, 128 * 128, device=dev).view(128, 128).contiguous()
+    ovf = torch.zeros(1, dtype=torch.int32, device=dev)
+    _lib.pack_weight(w, _lib.QT_LINEAR, _p(1 / 8, dev), _p(1.0, dev), None, _lib.W4, 128, 128, ovf)
+    assert ovf.item() == 1          # level 8 does not fit int4
+    ovf.zero_()
+    _lib.pack_weight(w, _lib.QT_LINEAR, _p(1 / 7, dev), _p(1.0, dev), None, _lib.W4, 128, 128, ovf)
+    assert ovf.item() == 0
+
+
+@pytest.mark.parametrize("conv", [dict(k=16, s=16, p=0, C=3, H=224), dict(k=3, s=1, p=1, C=16, H=20),
+                                  dict(k=3, s=2, p=1, C=5, H=17), dict(k=1, s=1, p=0, C=64, H=13)])
+def test_im2col_quant_vs_oracle(dev, conv):
+    g = torch.Generator().manual_seed(6)
+    B = 2
+    x = torch.randn(B, conv["C"], conv["H"], conv["H"], generator=g) * 0.5
+    d, qm = 1.0 / 127, 1.0
+    k, s, p = conv["k"], conv["s"], conv["p"]
+    K = conv["C"] * k * k
+    kpad = _round_up(K, 128)
+    OH = (conv["H"] + 2 * p - k) // s + 1
+    out = torch.empty((B * OH * OH, kpad), dtype=torch.int8, device=dev)
+    _lib.im2col_quant_i8(x.to(dev), k, k, s, s, p, p, 1, 1, _lib.QT_LINEAR, _p(d, dev), _p(qm, dev), None, 0, out,
+                         kpad)
+    codes = O.quant_codes(x, O.LINEAR, d, qm)
+    ref = F.unfold(codes, k, padding=p, stride=s).transpose(1, 2).reshape(B * OH * OH, K)
+    got = out.cpu()
+    assert torch.equal(got[:, :K].float(), ref)
+    assert (got[:, K:] == 0).all()
+
+
+@pytest.mark.parametrize("cols", [192, 768, 1000])
+def test_layernorm_quant_vs_oracle(dev, cols):
+    g = torch.Generator().manual_seed(8)
+    rows = 333
+    x = torch.randn(rows, cols, generator=g) * 2 + 0.3
+    gamma = torch.rand(cols, generator=g) + 0.5
+    beta = torch.randn(cols, generator=g) * 0.1
+    d, qm = 4.0 / 127, 4.0
+    kpad = _round_up(cols, 128)
+    out = torch.empty((rows, kpad), dtype=torch.int8, device=dev)
+    _lib.layernorm_quant_i8(x.to(dev), gamma.to(dev), beta.to(dev), 1e-6, _lib.QT_NONLINEAR, _p(d, dev),
+                            _p(qm, dev), _p(1.0, dev), 0, out, kpad)
+    ref = O.quant_codes(F.layer_norm(x, (cols,), gamma, beta, 1e-6), O.NONLINEAR, d, qm, 1.0)
+    got = out.cpu()
+    diff = (got[:, :cols].float() - ref).abs()
+    assert diff.max() <= 1
+    assert (diff > 0).float().mean() <= 5e-4
+    assert (got[:, cols:] == 0).all()

@@ -1,0 +1,224 @@
+"""GPU parity of the module surface and the ViT caller against the CPU oracle's fake-quant forward.
+
+North-star bar: logits match the reference fake-quant CPU forward on identical int4 weights within
+1e-3 relative (norm-wise). Module-level outputs (single layer) are held to 1e-5 relative.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from oracle import quant_oracle as O
+from quantized_vit_amd import _lib, vit_model
+from quantized_vit_amd.calibrate import build_quantized_vit, synthetic_images
+from quantized_vit_amd.quant_layers import (QuantizationMode, QuantizationType, QuantizeConv2d, QuantizeLinear,
+                                            initialize_quant_layer)
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / b.norm()).item()
+
+
+def _layer_q(m):
+    sd = m.state_dict()
+    qt = m.quant_type.value
+    return O.LayerQ.from_state(sd, "", qt, m.quant_mode.value)
+
+
+def _calibrated_linear(dev, k, n, qt, bits=4, t_act=1.0, seed=0):
+    torch.manual_seed(seed)
+    lin = nn.Linear(k, n)
+    q = QuantizeLinear.from_module(lin, quant_type=qt, quant_mode=QuantizationMode.WEIGHT_AND_ACTIVATION,
+                                   num_bits=bits).to(dev).eval()
+    with torch.no_grad():
+        q.q_m_act.fill_(2.0)
+        q.d_quant_act.fill_(np.exp(t_act * np.log(2.0)) / 127)
+        if hasattr(q, "t_quant_act"):
+            q.t_quant_act.fill_(t_act)
+    q.invalidate()
+    return q
+
+
+@pytest.mark.parametrize("qt", [QuantizationType.SYMMETRIC_LINEAR, QuantizationType.SYMMETRIC_NONLINEAR,
+                                QuantizationType.DGE])
+@pytest.mark.parametrize("k,n,bits", [(768, 3072, 4), (3072, 768, 4), (200, 77, 4), (768, 768, 6)])
+def test_quantize_linear_vs_oracle(dev, qt, k, n, bits):
+    q = _calibrated_linear(dev, k, n, qt, bits)
+    plan = q.quant_plan()
+    assert plan.int_path and plan.wfmt == (_lib.W4 if bits <= 4 else _lib.W8)
+    x = torch.randn(3, 70, k) * 0.7
+    with torch.no_grad():
+        y = q(x.to(dev))
+    ref = O.quantize_linear(x, q.weight.detach().cpu(), q.bias.detach().cpu(), _layer_q(q))
+    assert y.shape == ref.shape
+    assert rel(y, ref) < 1e-5
+
+
+def test_quantize_linear_reference_identity_limit_on_gpu(dev):
+    """OTO/tests/quantization/test_quant_layers.py:10-35 run on the GPU module (fp32 fake-quant path:
+    d = 1e-4, q_m = 10 gives 10^5 levels, beyond int8)."""
+    torch.manual_seed(0)
+    q = QuantizeLinear(256, 128, bias=True, d_quant_init=1e-4, t_quant_init=1.0, q_m_init=10.0).to(dev).eval()
+    lin = nn.Linear(256, 128).to(dev).eval()
+    with torch.no_grad():
+        lin.weight.copy_(torch.rand(128, 256))
+        q.weight.copy_(lin.weight)
+        q.bias.copy_(lin.bias)
+    x = torch.rand(1, 256, device=dev)
+    with torch.no_grad():
+        a, b = q(x), lin(x)
+    assert not q.quant_plan().int_path
+    assert torch.allclose(a, b, rtol=1e-4, atol=1e-8) or (a - b).abs().max().item() <= 1e-4
+
+
+def test_quantize_conv2d_reference_identity_limit_on_gpu(dev):
+    """test_quant_layers.py:38-78 on the GPU module."""
+    torch.manual_seed(0)
+    q = QuantizeConv2d(3, 64, 3, stride=1, padding=1, bias=True, d_quant_init=1e-4, q_m_init=10.0).to(dev).eval()
+    conv = nn.Conv2d(3, 64, 3, stride=1, padding=1, bias=True).to(dev).eval()
+    with torch.no_grad():
+        conv.weight.copy_(torch.rand(64, 3, 3, 3))
+        q.weight.copy_(conv.weight)
+        q.bias.copy_(conv.bias)
+        x = torch.rand(1, 3, 32, 32, device=dev)
+        a, b = q(x), conv(x)
+    assert torch.allclose(a, b, rtol=1e-4, atol=1e-8) or (a - b).abs().max().item() <= 1e-4
+
+
+@pytest.mark.parametrize("cfg", [dict(cin=3, cout=768, k=16, s=16, p=0, H=224),
+                                 dict(cin=16, cout=32, k=3, s=1, p=1, H=24), dict(cin=8, cout=20, k=3, s=2, p=1, H=15)])
+def test_quantize_conv2d_int_path_vs_oracle(dev, cfg):
+    torch.manual_seed(1)
+    conv = nn.Conv2d(cfg["cin"], cfg["cout"], cfg["k"], stride=cfg["s"], padding=cfg["p"], bias=True)
+    q = QuantizeConv2d.from_module(conv, quant_type=QuantizationType.SYMMETRIC_NONLINEAR,
+                                   quant_mode=QuantizationMode.WEIGHT_AND_ACTIVATION, num_bits=4).to(dev).eval()
+    with torch.no_grad():
+        q.q_m_act.fill_(1.0)
+        q.d_quant_act.fill_(1.0 / 127)
+    q.invalidate()
+    assert q.quant_plan().int_path
+    x = torch.rand(2, cfg["cin"], cfg["H"], cfg["H"]) * 2 - 1
+    with torch.no_grad():
+        y = q(x.to(dev))
+    ref = O.quantize_conv2d(x, q.weight.detach().cpu(), q.bias.detach().cpu(), _layer_q(q), stride=cfg["s"],
+                            padding=cfg["p"])
+    assert y.shape == ref.shape and y.is_contiguous()
+    assert rel(y, ref) < 1e-5
+
+
+def test_weight_only_mode_runs_fp_path(dev):
+    torch.manual_seed(2)
+    q = QuantizeLinear.from_module(nn.Linear(64, 32), quant_type=QuantizationType.SYMMETRIC_NONLINEAR,
+                                   num_bits=4).to(dev).eval()
+    x = torch.randn(5, 64)
+    with torch.no_grad():
+        y = q(x.to(dev))
+    assert not q.quant_plan().int_path
+    ref = O.quantize_linear(x, q.weight.detach().cpu(), q.bias.detach().cpu(), _layer_q(q))
+    assert rel(y, ref) < 1e-5
+
+
+def test_plan_cache_tracks_parameter_versions(dev):
+    q = _calibrated_linear(dev, 128, 64, QuantizationType.SYMMETRIC_NONLINEAR)
+    p1 = q.quant_plan()
+    assert q.quant_plan() is p1
+    with torch.no_grad():
+        q.weight.mul_(0.5)          # bumps the version counter
+    p2 = q.quant_plan()
+    assert p2 is not p1
+    x = torch.randn(4, 128)
+    with torch.no_grad():
+        y = q(x.to(dev))
+    assert rel(y, O.quantize_linear(x, q.weight.detach().cpu(), q.bias.detach().cpu(), _layer_q(q))) < 1e-5
+
+
+def _oracle_logits(model, cfg, img):
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    with torch.no_grad():
+        return O.vit_forward(sd, cfg, img)
+
+
+def test_vit_tiny_golden_logits(dev):
+    z = np.load(os.path.join(GOLDEN, "vit_tiny_b2_logits.npz"))
+    model = build_quantized_vit("vit_tiny_patch16_224", num_classes=int(z["num_classes"]), seed=int(z["seed"]),
+                                depth=int(z["depth"])).to(dev)
+    img = synthetic_images(int(z["batch"]), 224, seed=int(z["img_seed"]))
+    with torch.no_grad():
+        y = model(img.to(dev))
+    assert rel(y, torch.from_numpy(z["logits"])) < 1e-3
+
+
+@pytest.mark.parametrize("t_act", [1.0, 0.9])
+def test_vit_tiny_b8_vs_oracle(dev, t_act):
+    model = build_quantized_vit("vit_tiny_patch16_224", seed=3, t_act=t_act).to(dev)
+    assert all(b.fused_ok(torch.empty(1, 197, 192, device=dev)) for b in model.blocks)
+    cfg = O.ViTConfig(embed_dim=192, depth=12, num_heads=3)
+    img = synthetic_images(8, 224, seed=0)
+    with torch.no_grad():
+        y = model(img.to(dev))
+    ref = _oracle_logits(model, cfg, img)
+    r = rel(y, ref)
+    print(f"ViT-Tiny b8 t_act={t_act}: rel err {r:.3e}")
+    assert r < 1e-3
+
+
+def test_vit_fused_equals_modulewise(dev):
+    """The fused block pipeline vs running each module on its own (both on the GPU)."""
+    model = build_quantized_vit("vit_tiny_patch16_224", seed=4, depth=4).to(dev)
+    img = synthetic_images(4, 224, seed=2).to(dev)
+    with torch.no_grad():
+        fused = model(img)
+        x = model.patch_embed(img)
+        x = torch.cat((model.cls_token.expand(x.shape[0], -1, -1), x), dim=1) + model.pos_embed
+        for blk in model.blocks:
+            x = x + blk.attn(blk.norm1(x))
+            x = x + blk.mlp(blk.norm2(x))
+        ref = model.head(model.norm(x)[:, 0])
+    assert rel(fused, ref) < 1e-4
+
+
+def test_vit_base_b2_vs_oracle(dev):
+    model = build_quantized_vit("vit_base_patch16_224", seed=0).to(dev)
+    cfg = O.ViTConfig()
+    img = synthetic_images(2, 224, seed=5)
+    with torch.no_grad():
+        y = model(img.to(dev))
+    r = rel(y, _oracle_logits(model, cfg, img))
+    print(f"ViT-B/16 b2: rel err {r:.3e}")
+    assert r < 1e-3
+
+
+def test_pruned_shapes_vs_oracle(dev):
+    """Compressed checkpoints prune whole heads (qkv N = 3*h'*64) and arbitrary MLP neurons
+    (operator.py:1208-1246, pruning_compression.py:64-131,217-291)."""
+    torch.manual_seed(9)
+    m = vit_model.VisionTransformer(embed_dim=192, depth=2, num_heads=3, num_classes=37)
+    for blk in m.blocks:   # prune to 2 heads and 500 hidden neurons
+        a = blk.attn
+        a.qkv = nn.Linear(192, 3 * 2 * 64)
+        a.num_heads = 2
+        a.proj = nn.Linear(128, 192)
+        blk.mlp.fc1 = nn.Linear(192, 500)
+        blk.mlp.fc2 = nn.Linear(500, 192)
+    from quantized_vit_amd.calibrate import collect_input_absmax, set_activation_quant
+    from quantized_vit_amd.quant_model import model_to_quantize_model
+    m.eval()
+    img = synthetic_images(2, 224, seed=1)
+    absmax = collect_input_absmax(m, img)
+    m = model_to_quantize_model(m, num_bits=4, quant_mode="weight_and_activation")
+    set_activation_quant(m, absmax)
+    m = m.to(dev)
+    with torch.no_grad():
+        y = m(img.to(dev))
+    sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    cfg = O.ViTConfig(embed_dim=192, depth=2, num_heads=3, num_classes=37)
+    with torch.no_grad():
+        ref = O.vit_forward(sd, cfg, img)
+    assert rel(y, ref) < 1e-3
