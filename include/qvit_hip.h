@@ -67,7 +67,7 @@ extern "C" {
 #define QVIT_EPI_I32        4  /* C[m,n]  = acc                                      (int32, exact)  */
 
 /* Tile geometry the packed operands must be padded to. */
-#define QVIT_TILE_N  128   /* weight rows (out features) are padded to a multiple of this  */
+#define QVIT_TILE_N  256   /* weight rows (out features) are padded to a multiple of this  */
 #define QVIT_TILE_K  128   /* the reduction dim is padded to a multiple of this (zeros)    */
 
 const char* qvit_strerror(int code);

@@ -31,7 +31,7 @@ EPI_I8_GELU = 2
 EPI_I8 = 3
 EPI_I32 = 4
 
-TILE_N = 128
+TILE_N = 256
 TILE_K = 128
 
 _c_p = ctypes.c_void_p

@@ -2,30 +2,59 @@
 //   C[m, n] = epilogue( sum_k A[m, k] * W[n, k] ),  A = int8 activation codes, W = int4/int8 weight
 //   codes, exact int32 accumulation on v_mfma_i32_16x16x64_i8 (gfx950).
 //
-// Geometry (one workgroup = 256 threads = 4 waves):
-//   block tile 128 (n) x 128 (m), BK = 128 k per stage, two LDS stages (64 KiB) -> 2 blocks / CU.
-//   Waves form 2 (n) x 2 (m); each wave owns 64 n x 64 m = 4 x 4 MFMA tiles of 16 x 16.
-//   MFMA operand "A" (16 rows) = weights, operand "B" (16 cols) = activations, so the
-//   accumulator lane holds 4 consecutive weight rows of one activation row; the packer's row
-//   permutation (qvit_pack_weight) turns the 4 x 4 repeats into 16 consecutive output features.
-// Staging: activations and packed weights are register-staged (global_load_dwordx4) one stage
-//   ahead; int4 weights are sign-extended to int8 on the way into LDS (once per block, shared
-//   by both waves that read them). LDS rows are 128 B with the 16-B chunk index XOR-swizzled by
-//   (row >> 1) & 7, which makes the ds_read_b128 fragment reads conflict-free.
-// Grid: one block per output tile, blockIdx remapped so consecutive tiles (same activation
-//   panel, different weight panels) land on the same XCD / L2.
+// Geometry (one workgroup = 256 threads = 4 waves, 2 workgroups per CU):
+//   block tile 256 (n, weights) x 128 (m, activations); k advances in 64-deep stages.
+//   Wave w owns weight rows [64w, 64w+64) and all 128 activation rows: 4 x 8 MFMA tiles of 16x16.
+//   MFMA operand "A" (16 rows) = weights, operand "B" (16 cols) = activations.
+// Pipeline: a 4-deep LDS ring of stages (16 KiB each for int4 weights). Both operands go
+//   HBM/L2 -> LDS with global_load_lds_dwordx4 (issued from inline asm: no VGPRs, no ds_write, and
+//   no compiler-inserted vmcnt drains) three stages ahead; one counted `s_waitcnt vmcnt` + barrier per
+//   stage; the MFMA fragments of stage k+1 are read from LDS while the MFMAs of stage k run.
+//   int4 weights stay packed in LDS and are sign-extended after the ds_read_b64 fragment read
+//   (each unpacked fragment feeds 8 MFMAs).
+// LDS images are XOR-swizzled through the per-lane SOURCE address (the DMA writes lane-linear), so
+//   all fragment reads are bank-conflict free:
+//   activations (64-B rows):  16-B chunk c of row r at c ^ (((r >> 2) & 1) << 1)   (ds_read_b128)
+//   W4 weights  (32-B rows):   8-B chunk c of row r at c ^ (((r >> 3) & 1) << 1)   (ds_read_b64)
+//   W8 weights  (64-B rows):  as activations.
+// Epilogue: accumulators are staged through LDS (32 rows at a time per wave) and written back by a
+//   rolled loop in which 16 lanes own one contiguous 64-column row segment: 256-B coalesced fp32
+//   rows, 64-B int8 code rows, one inlined copy of the (GELU +) quantizer per element slot.
+// Grid: one block per output tile; blockIdx is remapped so that consecutive tiles (same activation
+//   panel, different weight panels) share an XCD and its L2.
+#include <type_traits>
+
 #include "qvit_common.h"
 
 namespace {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
-typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
-constexpr int BN = 128;      // weight rows per block
-constexpr int BM = 128;      // activation rows per block
-constexpr int BK = 128;      // k per stage (bytes of int8 per LDS row)
-constexpr int NT = 256;      // threads per block
-constexpr int TILE_BYTES = BN * BK;  // 16 KiB per operand per stage
+constexpr int BN = 256;    // weight rows per block
+constexpr int BK = 64;     // k per stage
+constexpr int KTILE = 128; // the API's K granularity (QVIT_TILE_K): stages come in pairs
+constexpr int RING = 4;    // LDS stages
+constexpr int AHEAD = 3;   // stages in flight ahead of the one being computed
+constexpr int EPI_LD = 68; // staged accumulator row pitch (ints): 64 + 4 pad
+constexpr int EPI_WAVE_INTS = 32 * EPI_LD;
+
+// WM = waves along m: WM = 1 -> 4 waves, tile 256 (n) x 128 (m), 2 blocks / CU;
+//                     WM = 2 -> 8 waves, tile 256 (n) x 256 (m), 1 block / CU (half the bytes per op)
+template <int WFMT, int WM>
+struct Geo {
+  static constexpr int NT = 256 * WM;
+  static constexpr int NWAVES = 4 * WM;
+  static constexpr int BM = 128 * WM;
+  static constexpr int XBYTES = BM * BK;                        // 8 / 16 KiB activation tile per stage
+  static constexpr int WROW = (WFMT == QVIT_W4) ? BK / 2 : BK;  // bytes per weight row per stage
+  static constexpr int WBYTES = BN * WROW;                      // 8 KiB (W4) / 16 KiB (W8)
+  static constexpr int STAGE = XBYTES + WBYTES;
+  static constexpr int LDS = RING * STAGE;
+  static constexpr int XPIECES = XBYTES / 1024 / NWAVES;        // 1-KiB DMA pieces per wave
+  static constexpr int WPIECES = WBYTES / 1024 / NWAVES;
+  static constexpr int DMA_PER_STAGE = XPIECES + WPIECES;       // per wave
+  static constexpr int MIN_BLOCKS = (WFMT == QVIT_W4 && WM == 1) ? 2 : 1;
+};
 
 QVIT_DEV uint32_t sext4_lo(uint32_t p) {
   const uint32_t x = p & 0x0F0F0F0Fu;
@@ -36,8 +65,33 @@ QVIT_DEV uint32_t sext4_hi(uint32_t p) {
   return ((x ^ 0x08080808u) + 0x78787878u) ^ 0x80808080u;
 }
 
-// byte offset of 16-byte chunk c of LDS row `row`
-QVIT_DEV int lds_off(int row, int c) { return row * BK + ((c ^ ((row >> 1) & 7)) << 4); }
+QVIT_DEV uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// One 1-KiB LDS-DMA piece: 64 lanes x 16 B from per-lane global addresses to lds_base + 16*lane.
+// Issued from asm so the compiler neither counts it nor drains vmcnt for it; M0 is saved/restored.
+QVIT_DEV void dma16(const void* gsrc, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_base)
+      : "memory");
+}
+
+// Wait until at most N of this wave's DMAs are in flight, retire its LDS reads, then barrier.
+// The LDS drain is the builtin (lgkmcnt(0) = 0xC07F on gfx9) so the compiler's wait-count model sees
+// it and does not re-drain lgkmcnt when the next stage's fragment reads are in flight.
+template <int N>
+QVIT_DEV void stage_sync() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
 
 struct EpiArgs {
   const float* d_act;
@@ -50,18 +104,32 @@ struct EpiArgs {
   int out_levels;
 };
 
-template <int WFMT, int EPI>
-__global__ __launch_bounds__(NT, 2) void gemm_kernel(const int8_t* __restrict__ A, int M, int K,
-                                                     int64_t lda, const void* __restrict__ Wp,
-                                                     int N, int npad, void* __restrict__ C,
-                                                     int64_t ldc, EpiArgs ep) {
-  __shared__ __attribute__((aligned(16))) int8_t smem[2 * 2 * TILE_BYTES];
+template <int WFMT>
+struct Frags {
+  v4i x[8];
+  uint2 w4[4];  // W4: packed 16 nibbles per lane
+  v4i w8[4];    // W8: 16 bytes per lane
+};
+
+// SHORT: K == 128 (two stages, all issued by the prologue); separate so that the steady-state
+// kernel has a single static tail (a runtime choice between tails makes the accumulators PHIs and
+// the register allocator then copies and spills them).
+template <int WFMT, int EPI, int WM, bool SHORT>
+__global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) void gemm_kernel(
+    const int8_t* __restrict__ A, int M, int K, int64_t lda, const int8_t* __restrict__ Wp, int N, int npad,
+    void* __restrict__ C, int64_t ldc, EpiArgs ep) {
+  using G = Geo<WFMT, WM>;
+  constexpr int BM = G::BM;
+  constexpr int XBYTES = G::XBYTES;
+  __shared__ __attribute__((aligned(16))) int8_t smem[G::LDS];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wn = wave & 1;   // weight-row half of the tile
-  const int wm = wave >> 1;  // activation-row half of the tile
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave & 3;   // weight rows [64 wn, 64 wn + 64)
+  const int wm = wave >> 2;  // activation rows [128 wm, 128 wm + 128)
+  const int fr = lane & 15;
+  const int fq = lane >> 4;
 
   // ---- tile assignment with a bijective XCD remap ----------------------------------------
   const int nb_n = npad / BN;
@@ -75,231 +143,254 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const int8_t* __restrict__ 
   const int n0 = tile_n * BN;
   const int m0 = tile_m * BM;
 
-  // ---- global -> register staging addresses ------------------------------------------------
-  // activations: 4 x 16 B per thread; row = (tid >> 3) + 32 i, chunk = tid & 7
-  const int xa_c = tid & 7;
-  const int8_t* xsrc[4];
-  int xdst[4];
+  // epilogue scalars are loaded before the main loop: no compiler VMEM op lands among the DMAs
+  float alpha = 0.f;
+  if (EPI != QVIT_EPI_I32) alpha = (*ep.d_act) * (*ep.d_wt);
+
+  // ---- LDS-DMA sources (per lane) and destinations (per wave) ---------------------------------
+  // activations: wave w stages rows [32w, 32w+32) as 2 pieces of 16 rows x 64 B
+  const int8_t* xsrc[G::XPIECES];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = (tid >> 3) + 32 * i;
+  for (int j = 0; j < G::XPIECES; ++j) {
+    const int row = 32 * wave + 16 * j + (lane >> 2);
     int gm = m0 + row;
-    gm = gm < M ? gm : M - 1;  // clamp the tail: loaded, never stored
-    xsrc[i] = A + (int64_t)gm * lda + xa_c * 16;
-    xdst[i] = lds_off(row, xa_c);
+    gm = gm < M ? gm : M - 1;  // clamp the tail: staged, never stored
+    const int logical = (lane & 3) ^ (((row >> 2) & 1) << 1);
+    xsrc[j] = A + (int64_t)gm * lda + logical * 16;
   }
-  // weights
-  constexpr int WLOADS = (WFMT == QVIT_W4) ? 2 : 4;
-  const int8_t* wsrc[WLOADS];
-  int wdst0[WLOADS], wdst1[WLOADS];
+  // weights: wave w stages rows [w * 256 / NWAVES, ...)
+  constexpr int WROWS_PER_PIECE = 1024 / G::WROW;  // 32 (W4) or 16 (W8)
+  constexpr int WROWS_PER_WAVE = BN / G::NWAVES;
   const int64_t wrow_bytes = (WFMT == QVIT_W4) ? (int64_t)K / 2 : (int64_t)K;
+  const int8_t* wsrc[G::WPIECES];
 #pragma unroll
-  for (int i = 0; i < WLOADS; ++i) {
+  for (int j = 0; j < G::WPIECES; ++j) {
+    int row, logical;
     if (WFMT == QVIT_W4) {
-      const int id = tid + NT * i;
-      const int row = id >> 2, c4 = id & 3;
-      wsrc[i] = reinterpret_cast<const int8_t*>(Wp) + (int64_t)(n0 + row) * wrow_bytes + c4 * 16;
-      wdst0[i] = lds_off(row, 2 * c4);
-      wdst1[i] = lds_off(row, 2 * c4 + 1);
+      row = WROWS_PER_WAVE * wave + WROWS_PER_PIECE * j + (lane >> 1);
+      logical = (lane & 1) ^ ((row >> 3) & 1);
     } else {
-      const int row = (tid >> 3) + 32 * i;
-      wsrc[i] = reinterpret_cast<const int8_t*>(Wp) + (int64_t)(n0 + row) * wrow_bytes + xa_c * 16;
-      wdst0[i] = lds_off(row, xa_c);
-      wdst1[i] = 0;
+      row = WROWS_PER_WAVE * wave + WROWS_PER_PIECE * j + (lane >> 2);
+      logical = (lane & 3) ^ (((row >> 2) & 1) << 1);
     }
+    wsrc[j] = Wp + (int64_t)(n0 + row) * wrow_bytes + logical * 16;
   }
+  const uint32_t lds0 = lds_addr(smem);
 
-  v4u xr[4];
-  v4u wr[WLOADS];
-
-  auto gload = [&](int kt) {
+  auto issue_stage = [&](int kt) {
+    const uint32_t sx = lds0 + (uint32_t)((kt % RING) * G::STAGE);
+    const uint32_t sw = sx + XBYTES;
     const int64_t kx = (int64_t)kt * BK;
     const int64_t kw = (WFMT == QVIT_W4) ? kx / 2 : kx;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) xr[i] = *reinterpret_cast<const v4u*>(xsrc[i] + kx);
+    for (int j = 0; j < G::XPIECES; ++j)
+      dma16(xsrc[j] + kx, __builtin_amdgcn_readfirstlane(sx + (32 * wave + 16 * j) * BK));
 #pragma unroll
-    for (int i = 0; i < WLOADS; ++i) wr[i] = *reinterpret_cast<const v4u*>(wsrc[i] + kw);
+    for (int j = 0; j < G::WPIECES; ++j)
+      dma16(wsrc[j] + kw,
+            __builtin_amdgcn_readfirstlane(sw + (WROWS_PER_WAVE * wave + WROWS_PER_PIECE * j) * G::WROW));
   };
-  auto lstore = [&](int stage) {
-    int8_t* sx = smem + stage * 2 * TILE_BYTES;
-    int8_t* sw = sx + TILE_BYTES;
+
+  // per-lane fragment offsets inside a stage
+  const int xoff = (128 * wm + fr) * BK + ((fq ^ (((fr >> 2) & 1) << 1)) << 4);
+  const int woff = (WFMT == QVIT_W4) ? (64 * wn + fr) * G::WROW + ((fq ^ (((fr >> 3) & 1) << 1)) << 3)
+                                     : (64 * wn + fr) * G::WROW + ((fq ^ (((fr >> 2) & 1) << 1)) << 4);
+
+  auto read_frags = [&](int kt, Frags<WFMT>& f) {
+    const int8_t* sx = smem + (kt % RING) * G::STAGE;
+    const int8_t* sw = sx + XBYTES;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) *reinterpret_cast<v4u*>(sx + xdst[i]) = xr[i];
+    for (int s = 0; s < 8; ++s) f.x[s] = *reinterpret_cast<const v4i*>(sx + xoff + s * 16 * BK);
 #pragma unroll
-    for (int i = 0; i < WLOADS; ++i) {
-      if (WFMT == QVIT_W4) {
-        const v4u p = wr[i];
-        *reinterpret_cast<v4u*>(sw + wdst0[i]) =
-            v4u{sext4_lo(p.x), sext4_hi(p.x), sext4_lo(p.y), sext4_hi(p.y)};
-        *reinterpret_cast<v4u*>(sw + wdst1[i]) =
-            v4u{sext4_lo(p.z), sext4_hi(p.z), sext4_lo(p.w), sext4_hi(p.w)};
-      } else {
-        *reinterpret_cast<v4u*>(sw + wdst0[i]) = wr[i];
-      }
+    for (int r = 0; r < 4; ++r) {
+      if (WFMT == QVIT_W4)
+        f.w4[r] = *reinterpret_cast<const uint2*>(sw + woff + r * 16 * G::WROW);
+      else
+        f.w8[r] = *reinterpret_cast<const v4i*>(sw + woff + r * 16 * G::WROW);
     }
   };
 
-  v4i acc[4][4];
+  v4i acc[4][8];
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
-    for (int s = 0; s < 4; ++s) acc[r][s] = v4i{0, 0, 0, 0};
+    for (int s = 0; s < 8; ++s) acc[r][s] = v4i{0, 0, 0, 0};
 
-  // fragment read offsets: row = base + 16 r + (lane & 15), chunk = 4 kk + (lane >> 4)
-  const int fr = lane & 15;
-  const int fq = lane >> 4;
-  const int wrow0 = wn * 64 + fr;
-  const int xrow0 = wm * 64 + fr;
-
-  const int nk = K / BK;
-  auto compute = [&](int cur) {
-    const int8_t* sx = smem + cur * 2 * TILE_BYTES;
-    const int8_t* sw = sx + TILE_BYTES;
+  auto mfma_stage = [&](const Frags<WFMT>& f) {
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      v4i wf[4], xf[4];
+    for (int r = 0; r < 4; ++r) {
+      v4i wf;
+      if (WFMT == QVIT_W4) {
+        const uint2 p = f.w4[r];
+        wf = v4i{(int)sext4_lo(p.x), (int)sext4_hi(p.x), (int)sext4_lo(p.y), (int)sext4_hi(p.y)};
+      } else {
+        wf = f.w8[r];
+      }
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        wf[r] = *reinterpret_cast<const v4i*>(sw + lds_off(wrow0 + 16 * r, 4 * kk + fq));
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-        xf[s] = *reinterpret_cast<const v4i*>(sx + lds_off(xrow0 + 16 * s, 4 * kk + fq));
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-          acc[r][s] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wf[r], xf[s], acc[r][s], 0, 0, 0);
+      for (int s = 0; s < 8; ++s) acc[r][s] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wf, f.x[s], acc[r][s], 0, 0, 0);
     }
   };
-  gload(0);
-  lstore(0);
+
+  // One pipeline step: stage kt is in registers (cur); bring stage kt+1 into registers (nxt).
+  // ISSUE: DMA stage kt+AHEAD; SYNC: this wave's DMAs allowed in flight when stage kt+1 is read
+  // (the stages newer than kt+1); READ: there is a stage kt+1. All three are compile-time per call
+  // site so the steady-state loop carries no branches: a join after conditional fragment reads makes
+  // the compiler drain lgkmcnt(0) in front of the MFMAs, serialising LDS latency with every stage.
+  constexpr int D = G::DMA_PER_STAGE;
+  const int nk = K / BK;  // even: K is a multiple of KTILE
+  auto step = [&](int kt, Frags<WFMT>& cur, Frags<WFMT>& nxt, auto issue, auto sync, auto read)
+                  __attribute__((always_inline)) {
+    // cur's fragment reads were issued a full stage of MFMAs ago; retiring them where the compiler
+    // can see it keeps the wait-count model exact at the MFMAs below.
+    // sched_barrier(0) fences keep the phases in this order: the steady loop is one basic block and
+    // the scheduler otherwise hoists nxt's unpack up to its reads (forcing a wait) across steps.
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (decltype(issue)::value) issue_stage(kt + AHEAD);
+    if constexpr (decltype(read)::value) {
+      stage_sync<decltype(sync)::value>();
+      read_frags(kt + 1, nxt);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_stage(cur);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  using Yes = std::true_type;
+  using No = std::false_type;
+  using Sync2 = std::integral_constant<int, 2 * D>;
+  using Sync1 = std::integral_constant<int, D>;
+  using Sync0 = std::integral_constant<int, 0>;
+
+  Frags<WFMT> fa, fb;
+#pragma unroll
+  for (int j = 0; j < AHEAD; ++j)
+    if (j < nk) issue_stage(j);
+  if (nk > 2) stage_sync<2 * D>();
+  else stage_sync<D>();
+  read_frags(0, fa);
+  int kt = 0;
+  if constexpr (!SHORT)
+  for (; kt + 5 <= nk; kt += 2) {  // both steps issue, two newer stages in flight
+    step(kt, fa, fb, Yes{}, Sync2{}, Yes{});
+    step(kt + 1, fb, fa, Yes{}, Sync2{}, Yes{});
+  }
+  if constexpr (!SHORT) {  // kt == nk - 4
+    step(kt, fa, fb, Yes{}, Sync2{}, Yes{});
+    step(kt + 1, fb, fa, No{}, Sync1{}, Yes{});
+    step(kt + 2, fa, fb, No{}, Sync0{}, Yes{});
+    step(kt + 3, fb, fa, No{}, Sync0{}, No{});
+  } else {  // nk == 2: both stages were issued by the prologue
+    step(0, fa, fb, No{}, Sync0{}, Yes{});
+    step(1, fb, fa, No{}, Sync0{}, No{});
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  // steady state: prefetch stage kt+1 into registers, compute stage kt, write kt+1 to LDS
-  for (int kt = 0; kt < nk - 1; ++kt) {
-    const int cur = kt & 1;
-    gload(kt + 1);
-    compute(cur);
-    lstore(cur ^ 1);
+
+  // ---- epilogue ---------------------------------------------------------------------------------
+  // acc[r][s][j] = C[m0 + 128 wm + 16 s + fr][n0 + 64 wn + 16 fq + 4 r + j] (weight rows pre-permuted)
+  int* stg = reinterpret_cast<int*>(smem) + wave * EPI_WAVE_INTS;
+  const int prow = lane >> 4;        // processing: row 4 i + prow of the staged 32
+  const int pcol = 4 * (lane & 15);  // 4 consecutive columns of the wave's 64
+  const int n = n0 + 64 * wn + pcol;
+  const bool nfull = n + 4 <= N;
+
+  float4 b4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  QParams qp;
+  if (EPI != QVIT_EPI_I32 && ep.bias != nullptr) b4 = *reinterpret_cast<const float4*>(ep.bias + n);
+  if (EPI == QVIT_EPI_I8 || EPI == QVIT_EPI_I8_GELU)
+    qp = load_qparams(ep.out_qtype, ep.out_d, ep.out_qm, ep.out_t, ep.out_levels);
+
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        *reinterpret_cast<v4i*>(stg + (16 * sl + fr) * EPI_LD + 16 * fq + 4 * r) = acc[r][2 * q + sl];
     __syncthreads();
-  }
-  compute((nk - 1) & 1);
-
-  // ---- epilogue -------------------------------------------------------------------------------
-  // acc[r][s][j] is C[m = m0 + 64 wm + 16 s + fr][n = n0 + 64 wn + 16 fq + 4 r + j]
-  const int nbase = n0 + wn * 64 + 16 * fq;
-  const bool nfull = nbase + 16 <= N;
-  if (EPI == QVIT_EPI_I32) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int m = m0 + wm * 64 + 16 * s + fr;
-      if (m >= M) continue;
-      int32_t* dst = reinterpret_cast<int32_t*>(C) + (int64_t)m * ldc + nbase;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (nfull) {
-          *reinterpret_cast<v4i*>(dst + 4 * r) = acc[r][s];
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (nbase + 4 * r + j < N) dst[4 * r + j] = acc[r][s][j];
-        }
-      }
-    }
-    return;
-  }
-
-  const float alpha = (*ep.d_act) * (*ep.d_wt);
-  float bv[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) bv[i] = 0.f;
-  if (ep.bias != nullptr) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float4 b4 = *reinterpret_cast<const float4*>(ep.bias + nbase + 4 * r);
-      bv[4 * r + 0] = b4.x; bv[4 * r + 1] = b4.y; bv[4 * r + 2] = b4.z; bv[4 * r + 3] = b4.w;
-    }
-  }
-
-  if (EPI == QVIT_EPI_F32 || EPI == QVIT_EPI_F32_RESID) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int m = m0 + wm * 64 + 16 * s + fr;
-      if (m >= M) continue;
-      float* dst = reinterpret_cast<float*>(C) + (int64_t)m * ldc + nbase;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float o[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = alpha * (float)acc[r][s][j] + bv[4 * r + j];
-        if (nfull) {
-          float4* d4 = reinterpret_cast<float4*>(dst + 4 * r);
-          if (EPI == QVIT_EPI_F32_RESID) {
-            const float4 old = *d4;
-            o[0] += old.x; o[1] += old.y; o[2] += old.z; o[3] += old.w;
+#pragma unroll 1
+    for (int i = 0; i < 8; ++i) {
+      const int row = 4 * i + prow;
+      const int m = m0 + 128 * wm + 32 * q + row;
+      const v4i a4 = *reinterpret_cast<const v4i*>(stg + row * EPI_LD + pcol);
+      if (m < M) {
+        if (EPI == QVIT_EPI_I32) {
+          int32_t* dst = reinterpret_cast<int32_t*>(C) + (int64_t)m * ldc + n;
+          if (nfull) {
+            *reinterpret_cast<v4i*>(dst) = a4;
+          } else {
+            for (int j = 0; j < 4; ++j)
+              if (n + j < N) dst[j] = a4[j];
           }
-          *d4 = make_float4(o[0], o[1], o[2], o[3]);
+        } else if (EPI == QVIT_EPI_F32 || EPI == QVIT_EPI_F32_RESID) {
+          float4 o = make_float4(alpha * (float)a4[0] + b4.x, alpha * (float)a4[1] + b4.y,
+                                 alpha * (float)a4[2] + b4.z, alpha * (float)a4[3] + b4.w);
+          float* dst = reinterpret_cast<float*>(C) + (int64_t)m * ldc + n;
+          if (nfull) {
+            if (EPI == QVIT_EPI_F32_RESID) {
+              const float4 old = *reinterpret_cast<const float4*>(dst);
+              o.x += old.x; o.y += old.y; o.z += old.z; o.w += old.w;
+            }
+            *reinterpret_cast<float4*>(dst) = o;
+          } else {
+            const float ov[4] = {o.x, o.y, o.z, o.w};
+            for (int j = 0; j < 4; ++j)
+              if (n + j < N) dst[j] = (EPI == QVIT_EPI_F32_RESID) ? dst[j] + ov[j] : ov[j];
+          }
         } else {
+          const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
+          float v[4], k[4];
+          bool need[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            if (nbase + 4 * r + j < N) {
-              if (EPI == QVIT_EPI_F32_RESID) dst[4 * r + j] += o[j];
-              else dst[4 * r + j] = o[j];
-            }
+            v[j] = alpha * (float)a4[j] + bb[j];
+            if (EPI == QVIT_EPI_I8_GELU) v[j] = gelu_ref(v[j]);
+            k[j] = quant_fast(v[j], qp, need[j]);
+          }
+          if (__any(need[0] | need[1] | need[2] | need[3])) {  // rare: near-tie elements
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (need[j]) k[j] = quant_fixup(v[j], qp);
+          }
+          uint32_t word = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) word |= ((uint32_t)(uint8_t)to_i8_sat(k[j])) << (8 * j);
+          int8_t* dst = reinterpret_cast<int8_t*>(C) + (int64_t)m * ldc + n;
+          if (nfull) {
+            *reinterpret_cast<uint32_t*>(dst) = word;
+          } else {
+            for (int j = 0; j < 4; ++j)
+              if (n + j < N) dst[j] = (int8_t)((word >> (8 * j)) & 0xff);
           }
         }
       }
     }
-    return;
-  }
-
-  // int8-code epilogues: the next layer's quantizer applied to (optionally GELU of) the output
-  const QParams qp = load_qparams(ep.out_qtype, ep.out_d, ep.out_qm, ep.out_t, ep.out_levels);
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int m = m0 + wm * 64 + 16 * s + fr;
-    if (m >= M) continue;
-    int8_t* dst = reinterpret_cast<int8_t*>(C) + (int64_t)m * ldc + nbase;
-    uint32_t words[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      uint32_t wv = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float v = alpha * (float)acc[r][s][j] + bv[4 * r + j];
-        if (EPI == QVIT_EPI_I8_GELU) v = gelu_erf(v);
-        wv |= ((uint32_t)(uint8_t)to_i8_sat(quant_code(v, qp))) << (8 * j);
-      }
-      words[r] = wv;
-    }
-    if (nfull) {
-      *reinterpret_cast<uint4*>(dst) = make_uint4(words[0], words[1], words[2], words[3]);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 16; ++i)
-        if (nbase + i < N) dst[i] = (int8_t)((words[i >> 2] >> (8 * (i & 3))) & 0xff);
-    }
+    __syncthreads();
   }
 }
 
 template <int WFMT, int EPI>
-int launch(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int64_t N,
-           int64_t npad, void* C, int64_t ldc, const EpiArgs& ep, hipStream_t stream) {
-  const int64_t nblk = (npad / BN) * ((M + BM - 1) / BM);
-  hipLaunchKernelGGL((gemm_kernel<WFMT, EPI>), dim3((unsigned)nblk), dim3(NT), 0, stream, A, (int)M,
-                     (int)K, lda, Wp, (int)N, (int)npad, C, ldc, ep);
+int launch(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int64_t N, int64_t npad,
+           void* C, int64_t ldc, const EpiArgs& ep, hipStream_t stream) {
+  using G = Geo<WFMT, 1>;
+  const int64_t nblk = (npad / BN) * ((M + G::BM - 1) / G::BM);
+  const int8_t* W = reinterpret_cast<const int8_t*>(Wp);
+  if (K == KTILE)
+    hipLaunchKernelGGL((gemm_kernel<WFMT, EPI, 1, true>), dim3((unsigned)nblk), dim3(G::NT), 0, stream, A, (int)M,
+                       (int)K, lda, W, (int)N, (int)npad, C, ldc, ep);
+  else
+    hipLaunchKernelGGL((gemm_kernel<WFMT, EPI, 1, false>), dim3((unsigned)nblk), dim3(G::NT), 0, stream, A, (int)M,
+                       (int)K, lda, W, (int)N, (int)npad, C, ldc, ep);
   return qvit_hip_status(hipGetLastError());
 }
 
 template <int WFMT>
-int dispatch_epi(int epilogue, const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp,
-                 int64_t N, int64_t npad, void* C, int64_t ldc, const EpiArgs& ep,
-                 hipStream_t stream) {
+int dispatch_epi(int epilogue, const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int64_t N,
+                 int64_t npad, void* C, int64_t ldc, const EpiArgs& ep, hipStream_t stream) {
   switch (epilogue) {
     case QVIT_EPI_F32: return launch<WFMT, QVIT_EPI_F32>(A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
-    case QVIT_EPI_F32_RESID:
-      return launch<WFMT, QVIT_EPI_F32_RESID>(A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
-    case QVIT_EPI_I8_GELU:
-      return launch<WFMT, QVIT_EPI_I8_GELU>(A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
+    case QVIT_EPI_F32_RESID: return launch<WFMT, QVIT_EPI_F32_RESID>(A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
+    case QVIT_EPI_I8_GELU: return launch<WFMT, QVIT_EPI_I8_GELU>(A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
     case QVIT_EPI_I8: return launch<WFMT, QVIT_EPI_I8>(A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
     case QVIT_EPI_I32: return launch<WFMT, QVIT_EPI_I32>(A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
     default: return QVIT_EINVAL;
@@ -308,25 +399,23 @@ int dispatch_epi(int epilogue, const int8_t* A, int64_t M, int64_t K, int64_t ld
 
 }  // namespace
 
-extern "C" int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp,
-                         int wfmt, int64_t N, int64_t npad, const float* d_act, const float* d_wt,
-                         const float* bias, int epilogue, void* C, int64_t ldc, int out_qtype,
-                         const float* out_d, const float* out_qm, const float* out_t,
-                         int out_levels, hipStream_t stream) {
+extern "C" int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int wfmt, int64_t N,
+                         int64_t npad, const float* d_act, const float* d_wt, const float* bias, int epilogue,
+                         void* C, int64_t ldc, int out_qtype, const float* out_d, const float* out_qm,
+                         const float* out_t, int out_levels, hipStream_t stream) {
   if (!A || !Wp || !C) return QVIT_ENULL;
   if (wfmt != QVIT_W4 && wfmt != QVIT_W8) return QVIT_EINVAL;
-  if (M < 0 || K <= 0 || K % BK || lda < K || N <= 0 || npad < N || npad % BN) return QVIT_EINVAL;
+  if (M < 0 || K <= 0 || K % KTILE || lda < K || N <= 0 || npad < N || npad % BN) return QVIT_EINVAL;
   if (M > INT32_MAX / 2 || npad > INT32_MAX / 2 || K > (1 << 24)) return QVIT_EINVAL;
   if ((lda % 16) || (((uintptr_t)A) & 15) || (((uintptr_t)Wp) & 15)) return QVIT_EALIGN;
-  const bool i8out = epilogue == QVIT_EPI_I8 || epilogue == QVIT_EPI_I8_GELU;
   if (epilogue < QVIT_EPI_F32 || epilogue > QVIT_EPI_I32) return QVIT_EINVAL;
+  const bool i8out = epilogue == QVIT_EPI_I8 || epilogue == QVIT_EPI_I8_GELU;
   if (ldc < N) return QVIT_EINVAL;
   if (i8out) {
-    if ((ldc % 16) || (((uintptr_t)C) & 15)) return QVIT_EALIGN;
+    if ((ldc % 4) || (((uintptr_t)C) & 3)) return QVIT_EALIGN;
     const int q = out_qtype & 0xff;
     if (q != QVIT_QT_LINEAR && q != QVIT_QT_NONLINEAR && q != QVIT_QT_ULTRA_ACT) return QVIT_EINVAL;
-    if (q == QVIT_QT_ULTRA_ACT ? (out_levels < 1 || out_levels > 127) : (!out_d || !out_qm))
-      return QVIT_EINVAL;
+    if (q == QVIT_QT_ULTRA_ACT ? (out_levels < 1 || out_levels > 127) : (!out_d || !out_qm)) return QVIT_EINVAL;
   } else {
     if ((ldc % 4) || (((uintptr_t)C) & 15)) return QVIT_EALIGN;
   }

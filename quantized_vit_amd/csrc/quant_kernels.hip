@@ -208,6 +208,60 @@ QVIT_DEV float wave_sum(float v) {
   return v;
 }
 
+// Register-resident row: cols % 4 == 0, cols <= 256 * NV. One HBM read of the row, two-pass
+// statistics from registers (mean, then sum of squared deviations), one int8 write.
+template <int NV>
+__global__ __launch_bounds__(kThreads) void layernorm_quant_reg_kernel(
+    const float* __restrict__ x, int64_t rows, int64_t cols, int64_t ldx, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, int qtype, const float* d, const float* qm, const float* t,
+    int levels, int8_t* __restrict__ codes, int64_t ldc, int64_t kpad) {
+  const QParams p = load_qparams(qtype, d, qm, t, levels);
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  if (r >= rows) return;
+  const float* xr = x + r * ldx;
+  float4 v[NV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int64_t c = 4 * (lane + 64 * i);
+    v[i] = (c < cols) ? *reinterpret_cast<const float4*>(xr + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  }
+  const float mean = wave_sum(s) / (float)cols;
+  float s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int64_t c = 4 * (lane + 64 * i);
+    if (c < cols) {
+      const float a = v[i].x - mean, b = v[i].y - mean, cc = v[i].z - mean, dd = v[i].w - mean;
+      s2 += (a * a + b * b) + (cc * cc + dd * dd);
+    }
+  }
+  const float var = wave_sum(s2) / (float)cols;
+  const float rstd = 1.0f / sqrtf(var + eps);
+  int8_t* cr = codes + r * ldc;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int64_t c = 4 * (lane + 64 * i);
+    if (c < cols) {
+      const float4 g = gamma ? *reinterpret_cast<const float4*>(gamma + c) : make_float4(1.f, 1.f, 1.f, 1.f);
+      const float4 b = beta ? *reinterpret_cast<const float4*>(beta + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float y0 = (v[i].x - mean) * rstd * g.x + b.x;
+      const float y1 = (v[i].y - mean) * rstd * g.y + b.y;
+      const float y2 = (v[i].z - mean) * rstd * g.z + b.z;
+      const float y3 = (v[i].w - mean) * rstd * g.w + b.w;
+      const uint32_t word = (uint32_t)(uint8_t)to_i8_sat(quant_code(y0, p)) |
+                            ((uint32_t)(uint8_t)to_i8_sat(quant_code(y1, p)) << 8) |
+                            ((uint32_t)(uint8_t)to_i8_sat(quant_code(y2, p)) << 16) |
+                            ((uint32_t)(uint8_t)to_i8_sat(quant_code(y3, p)) << 24);
+      *reinterpret_cast<uint32_t*>(cr + c) = word;
+    }
+  }
+  for (int64_t c = cols + lane; c < kpad; c += 64) cr[c] = 0;
+}
+
+// General rows (any cols / stride): re-reads the row from cache for each pass.
 __global__ __launch_bounds__(kThreads) void layernorm_quant_kernel(
     const float* __restrict__ x, int64_t rows, int64_t cols, int64_t ldx,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps, int qtype,
@@ -217,56 +271,24 @@ __global__ __launch_bounds__(kThreads) void layernorm_quant_kernel(
   const int lane = threadIdx.x & 63;
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  const bool vec = ((cols & 3) == 0) && ((ldx & 3) == 0) && ((((uintptr_t)x) & 15) == 0);
   for (int64_t r = wave; r < rows; r += nwaves) {
     const float* xr = x + r * ldx;
     float s = 0.f;
-    if (vec) {
-      for (int64_t c = lane * 4; c < cols; c += 256) {
-        float4 f = *reinterpret_cast<const float4*>(xr + c);
-        s += (f.x + f.y) + (f.z + f.w);
-      }
-    } else {
-      for (int64_t c = lane; c < cols; c += 64) s += xr[c];
-    }
+    for (int64_t c = lane; c < cols; c += 64) s += xr[c];
     const float mean = wave_sum(s) / (float)cols;
     float s2 = 0.f;
-    if (vec) {
-      for (int64_t c = lane * 4; c < cols; c += 256) {
-        float4 f = *reinterpret_cast<const float4*>(xr + c);
-        const float a = f.x - mean, b = f.y - mean, cc = f.z - mean, dd = f.w - mean;
-        s2 += (a * a + b * b) + (cc * cc + dd * dd);
-      }
-    } else {
-      for (int64_t c = lane; c < cols; c += 64) {
-        const float a = xr[c] - mean;
-        s2 += a * a;
-      }
+    for (int64_t c = lane; c < cols; c += 64) {
+      const float a = xr[c] - mean;
+      s2 += a * a;
     }
     const float var = wave_sum(s2) / (float)cols;
     const float rstd = 1.0f / sqrtf(var + eps);
     int8_t* cr = codes + r * ldc;
-    if (vec) {
-      for (int64_t c = lane * 4; c < cols; c += 256) {
-        float4 f = *reinterpret_cast<const float4*>(xr + c);
-        float vv[4] = {f.x, f.y, f.z, f.w};
-        uint32_t word = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float y = (vv[i] - mean) * rstd;
-          if (gamma) y = y * gamma[c + i];
-          if (beta) y = y + beta[c + i];
-          word |= ((uint32_t)(uint8_t)to_i8_sat(quant_code(y, p))) << (8 * i);
-        }
-        *reinterpret_cast<uint32_t*>(cr + c) = word;
-      }
-    } else {
-      for (int64_t c = lane; c < cols; c += 64) {
-        float y = (xr[c] - mean) * rstd;
-        if (gamma) y = y * gamma[c];
-        if (beta) y = y + beta[c];
-        cr[c] = to_i8_sat(quant_code(y, p));
-      }
+    for (int64_t c = lane; c < cols; c += 64) {
+      float y = (xr[c] - mean) * rstd;
+      if (gamma) y = y * gamma[c];
+      if (beta) y = y + beta[c];
+      cr[c] = to_i8_sat(quant_code(y, p));
     }
     for (int64_t c = cols + lane; c < kpad; c += 64) cr[c] = 0;
   }
@@ -392,10 +414,22 @@ int qvit_layernorm_quant_i8(const float* x, int64_t rows, int64_t cols, int64_t 
   if (rows < 0 || cols <= 0 || ldx < cols || kpad < cols || ldc < kpad) return QVIT_EINVAL;
   if (((ldc & 3) != 0) || (((uintptr_t)codes) & 3)) return QVIT_EALIGN;
   if (rows == 0) return QVIT_OK;
-  const int64_t work = rows * 64;
-  hipLaunchKernelGGL(layernorm_quant_kernel, dim3(grid_for(work, kThreads)), dim3(kThreads), 0,
-                     stream, x, rows, cols, ldx, gamma, beta, eps, qtype, d_quant, q_m, t_quant,
-                     levels, codes, ldc, kpad);
+  const bool reg = ((cols & 3) == 0) && ((ldx & 3) == 0) && ((((uintptr_t)x) & 15) == 0) &&
+                   (!gamma || (((uintptr_t)gamma) & 15) == 0) && (!beta || (((uintptr_t)beta) & 15) == 0);
+  const int nv = (int)((cols + 255) / 256);
+  const dim3 grid((unsigned)((rows + 3) / 4));
+#define QVIT_LN_REG(NV)                                                                                   \
+  hipLaunchKernelGGL(layernorm_quant_reg_kernel<NV>, grid, dim3(kThreads), 0, stream, x, rows, cols, ldx, \
+                     gamma, beta, eps, qtype, d_quant, q_m, t_quant, levels, codes, ldc, kpad)
+  if (reg && nv <= 1) QVIT_LN_REG(1);
+  else if (reg && nv <= 2) QVIT_LN_REG(2);
+  else if (reg && nv <= 3) QVIT_LN_REG(3);
+  else if (reg && nv <= 4) QVIT_LN_REG(4);
+  else if (reg && nv <= 8) QVIT_LN_REG(8);
+  else
+    hipLaunchKernelGGL(layernorm_quant_kernel, dim3(grid_for(rows * 64, kThreads)), dim3(kThreads), 0, stream, x,
+                       rows, cols, ldx, gamma, beta, eps, qtype, d_quant, q_m, t_quant, levels, codes, ldc, kpad);
+#undef QVIT_LN_REG
   return qvit_hip_status(hipGetLastError());
 }
 

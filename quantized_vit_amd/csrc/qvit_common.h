@@ -18,6 +18,14 @@
 // the careful (IEEE division + ocml exp/log) sequence. Results must be identical either way.
 #define QVIT_QT_FORCE_CAREFUL 0x100
 
+// fp32 log / exp rounded from double precision: the correctly rounded fp32 result except for
+// double-rounding ties (~2^-29). torch's CPU kernels (Sleef u10) return the correctly rounded
+// value for all but ~0.1% (log) / ~0.3% (exp) of inputs, so this matches the reference far more
+// often than the fp32 ocml sequence (v_log_f32/v_exp_f32 based, a few ulp).
+QVIT_DEV float log_cr(float a) { return (float)log((double)a); }
+QVIT_DEV float exp_cr(float a) { return (float)exp((double)a); }
+
+
 struct QParams {
   int qtype;      // QVIT_QT_*
   int careful;    // 1 -> always take the careful path
@@ -45,60 +53,65 @@ QVIT_DEV QParams load_qparams(int qtype, const float* d, const float* qm, const 
   if (p.qtype == QVIT_QT_LINEAR) {
     p.L = rintf(fabsf(p.qm) / p.d);
   } else {
-    p.L = rintf(expf(p.t * logf(fabsf(p.qm) + 1e-6f)) / p.d);
+    p.L = rintf(exp_cr(p.t * log_cr(fabsf(p.qm) + 1e-6f)) / p.d);
   }
   return p;
 }
 
-// Careful magnitude code for 0 < a < q_m: the reference's op sequence in fp32 with IEEE division
-// (hipcc default: correctly rounded fp32 divide) and ocml exp/log.
+// Careful magnitude code for 0 < a < q_m: the reference's op sequence
+//   exp(t * log(a)) (fp32 values at every step), IEEE fp32 division, round-half-even.
+// Out of line: it runs for a small fraction of elements (near rounding ties), and inlining its
+// double-precision exp/log into every unrolled call site bloats kernels past the I-cache.
+__device__ __noinline__ float code_mag_careful_ool(float a, int linear, float t, float d) {
+  float pw = linear ? a : exp_cr(t * log_cr(a));
+  return rintf(pw / d);
+}
 QVIT_DEV float code_mag_careful(float a, const QParams& p) {
-  float pw = (p.qtype == QVIT_QT_LINEAR) ? a : expf(p.t * logf(a));
-  return rintf(pw / p.d);
+  return code_mag_careful_ool(a, p.qtype == QVIT_QT_LINEAR, p.t, p.d);
 }
 
-// Guarded fast path: an approximate quotient q; if q is provably far from a rounding boundary
-// (x.5) the rounded result equals the careful one, otherwise fall back to the careful sequence.
-// Error budget: q carries <= ~3 ulp (linear) or (|t ln a| + 3) ulp (nonlinear) of relative error;
-// the margin below is 8x that, so both paths round identically whenever the fast one is taken.
-QVIT_DEV float code_mag(float a, const QParams& p) {
-  if (p.careful) return code_mag_careful(a, p);
+// Guarded fast path, branch-free: an approximate quotient q; if q is provably far from a rounding
+// tie (x.5) the rounded result equals the careful one. Otherwise `need` is set and the caller runs
+// code_mag_careful for that element (rare: ~1e-4 of elements). Error budget: q carries <= ~3 ulp
+// (linear) or (|t ln a| + 3) ulp (nonlinear) of relative error; the margin is 8x that.
+// Returns the signed code (integer-valued float); x == 0 and NaN give 0.
+QVIT_DEV float quant_fast(float x, const QParams& p, bool& need) {
+  if (p.qtype == QVIT_QT_ULTRA_ACT) {
+    // uniform_quantize(clamp(x,0,1)) with n = 2^b - 1: round(c * n) (quant_ultra.py:18-19,71)
+    need = false;
+    return rintf(fminf(fmaxf(x, 0.f), 1.f) * p.levels);
+  }
+  const float a = fabsf(x);
   float q, relerr;
   if (p.qtype == QVIT_QT_LINEAR) {
     q = a * p.inv_d;
     relerr = 32.f * 1.1920929e-7f;
   } else {
-    if (!(a > 1e-30f)) return code_mag_careful(a, p);  // hw log2 flushes denormals
-    float lg = __builtin_amdgcn_logf(a);                 // v_log_f32 (log2)
-    float e = p.t * lg;
-    float pw = (p.t == 1.f) ? a : __builtin_amdgcn_exp2f(e);  // v_exp_f32
+    // |t * ln(a)| bound from the binary exponent (no transcendental on the t == 1 path)
+    const float eb = fabsf(p.t) * (float)(abs(__builtin_amdgcn_frexp_expf(a)) + 1);
+    const float pw = (p.t == 1.f) ? a : __builtin_amdgcn_exp2f(p.t * __builtin_amdgcn_logf(a));
     q = pw * p.inv_d;
-    relerr = (fabsf(e) * 0.6931472f + 4.f) * 8.f * 1.1920929e-7f;
+    relerr = (eb * 0.6931472f + 4.f) * 8.f * 1.1920929e-7f;
   }
-  float aq = fabsf(q);
-  float f = aq - floorf(aq);
-  if (fabsf(f - 0.5f) > aq * relerr + 1e-37f) return rintf(q);
-  return code_mag_careful(a, p);
+  const float f = q - floorf(q);
+  const bool in_range = (a < p.qm) && (a > 0.f);
+  const bool tiny = (p.qtype == QVIT_QT_NONLINEAR) && !(a > 1e-30f);  // hw log2 flushes denormals
+  need = in_range && ((fabsf(f - 0.5f) <= fabsf(q) * relerr + 1e-37f) || tiny || p.careful);
+  float k = (a >= p.qm) ? p.L : rintf(q);  // saturation mask (:67, :159)
+  k = copysignf(k, x);                     // output = sign(input) * output (:68, :160)
+  return (a > 0.f) ? k : 0.f;              // zero mask (:66, :158); NaN -> 0
+}
+
+// Careful result for an element flagged by quant_fast.
+QVIT_DEV float quant_fixup(float x, const QParams& p) {
+  return copysignf(code_mag_careful(fabsf(x), p), x);
 }
 
 // Signed code k (as an integer-valued float), v_ref = d * k.
 QVIT_DEV float quant_code(float x, const QParams& p) {
-  if (p.qtype == QVIT_QT_ULTRA_ACT) {
-    // uniform_quantize(clamp(x,0,1)) with n = 2^b - 1: round(c * n) (quant_ultra.py:18-19,71)
-    float c = fminf(fmaxf(x, 0.f), 1.f);
-    return rintf(c * p.levels);
-  }
-  float a = fabsf(x);
-  float k;
-  if (a >= p.qm) {
-    k = p.L;                     // output[input_abs >= q_m] = d*round(range_pow/d)   (:67, :159)
-  } else if (a > 0.f) {
-    k = code_mag(a, p);
-  } else {
-    k = 0.f;                     // output[input_abs <= q_s] = 0                      (:66, :158)
-  }
-  // output = sign(input) * output (:68, :160); sign(0) = 0. NaN inputs map to 0.
-  return (x > 0.f) ? k : ((x < 0.f) ? -k : 0.f);
+  bool need;
+  const float k = quant_fast(x, p, need);
+  return need ? quant_fixup(x, p) : k;
 }
 
 // The reference's fp32 fake-quant value for the same element (d * k, rounded once in fp32,
@@ -116,9 +129,18 @@ QVIT_DEV int8_t to_i8_sat(float k) {
   return (int8_t)(int)k;
 }
 
-// nn.GELU() (approximate='none'): x * 0.5 * (1 + erf(x / sqrt(2)))   (vit_model.py:242,173)
-QVIT_DEV float gelu_erf(float x) {
-  return x * 0.5f * (1.0f + erff(x * 0.70710678118654752440f));
+// nn.GELU() (approximate='none', vit_model.py:242,173) as the reference computes it on the CPU:
+// x * 0.5 * (1 + erf(x * M_SQRT1_2)) with torch's vectorized erf = Abramowitz-Stegun 7.1.26
+// (ATen/cpu/vec/vec512/vec512_float.h, Vectorized<float>::erf): sign(u) * (1 - r(t) t exp(-u^2)),
+// t = 1 / (1 + 0.3275911 |u|). Branch-free, one exp. (|erf error| <= 1.5e-7, like the reference.)
+QVIT_DEV float gelu_ref(float x) {
+  const float u = x * 0.70710678f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, fabsf(u), 1.0f));
+  const float r = fmaf(fmaf(fmaf(fmaf(1.061405429f, t, -1.453152027f), t, 1.421413741f), t, -0.284496736f), t,
+                       0.254829592f);
+  const float e = __expf(-(u * u));
+  const float erf_abs = fmaf(-e * t, r, 1.0f);
+  return x * 0.5f * (1.0f + copysignf(erf_abs, u));
 }
 
 static inline int qvit_hip_status(hipError_t e) {

@@ -1,0 +1,61 @@
+"""Batch-sharded inference across the GPUs of one node (BASELINE.json configs[2]).
+
+Images are independent in the reference's eval forward (no BatchNorm in the ViT, LayerNorm is per
+token), so the path partitions by image: rank r owns global images [r*b, (r+1)*b) and holds a full
+model replica (ViT-B int4 ~ 43 MB). The only exchange is one all-gather of the fp32 logits
+(RCCL over xGMI with backend "nccl"; ~1 MB per rank at b=256, C=1000). One process per GPU.
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def shard_bounds(global_batch: int, world: int, rank: int) -> Tuple[int, int]:
+    """[start, end) of rank's images; the first global_batch % world ranks get one extra image."""
+    base, extra = divmod(global_batch, world)
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+def gather_logits(local: torch.Tensor, global_batch: int, group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
+    """All-gathers every rank's [b_r, C] logits into [global_batch, C] in global image order.
+    Ragged shards are padded to the largest shard for the collective and trimmed afterwards."""
+    world = dist.get_world_size(group)
+    if world == 1:
+        return local
+    per = -(-global_batch // world)
+    C = local.shape[1]
+    buf = local
+    if local.shape[0] != per:
+        buf = torch.zeros((per, C), dtype=local.dtype, device=local.device)
+        buf[: local.shape[0]] = local
+    out = torch.empty((world * per, C), dtype=local.dtype, device=local.device)
+    dist.all_gather_into_tensor(out, buf.contiguous(), group=group)
+    if per * world == global_batch:
+        return out
+    keep = []
+    for r in range(world):
+        s, e = shard_bounds(global_batch, world, r)
+        keep.append(out[r * per: r * per + (e - s)])
+    return torch.cat(keep, 0)
+
+
+class ShardedInference:
+    """Runs `model` on this rank's shard of a global batch and returns all logits on every rank."""
+
+    def __init__(self, model: Callable[[torch.Tensor], torch.Tensor], group: Optional[dist.ProcessGroup] = None):
+        self.model = model
+        self.group = group
+
+    @torch.no_grad()
+    def __call__(self, global_images: torch.Tensor) -> torch.Tensor:
+        world = dist.get_world_size(self.group) if dist.is_initialized() else 1
+        rank = dist.get_rank(self.group) if dist.is_initialized() else 0
+        s, e = shard_bounds(global_images.shape[0], world, rank)
+        local = self.model(global_images[s:e])
+        if world == 1:
+            return local
+        return gather_logits(local, global_images.shape[0], self.group)

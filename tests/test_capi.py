@@ -55,16 +55,16 @@ def test_constants_match_header():
 def test_argument_validation_without_launch(lib):
     fake = ctypes.c_void_p(0x1000)   # never dereferenced: validation rejects before any launch
     # NULL operands
-    assert lib.qvit_gemm(None, 16, 128, 128, fake, 4, 16, 128, fake, fake, None, 0, fake, 16, 0, None, None,
+    assert lib.qvit_gemm(None, 16, 128, 128, fake, 4, 16, 256, fake, fake, None, 0, fake, 16, 0, None, None,
                          None, 0, None) == -3
     # K not a multiple of the tile
-    assert lib.qvit_gemm(fake, 16, 100, 128, fake, 4, 16, 128, fake, fake, None, 0, fake, 16, 0, None, None,
+    assert lib.qvit_gemm(fake, 16, 100, 128, fake, 4, 16, 256, fake, fake, None, 0, fake, 16, 0, None, None,
                          None, 0, None) == -1
     # bad weight format
-    assert lib.qvit_gemm(fake, 16, 128, 128, fake, 5, 16, 128, fake, fake, None, 0, fake, 16, 0, None, None,
+    assert lib.qvit_gemm(fake, 16, 128, 128, fake, 5, 16, 256, fake, fake, None, 0, fake, 16, 0, None, None,
                          None, 0, None) == -1
     # misaligned activation stride
-    assert lib.qvit_gemm(fake, 16, 128, 136, fake, 4, 16, 128, fake, fake, None, 0, fake, 16, 0, None, None,
+    assert lib.qvit_gemm(fake, 16, 128, 136, fake, 4, 16, 256, fake, fake, None, 0, fake, 16, 0, None, None,
                          None, 0, None) == -2
     # bad quantizer enum
     assert lib.qvit_quantize_act_i8(fake, 4, 16, 16, 7, fake, fake, None, 0, fake, 16, 16, None) == -1
@@ -73,6 +73,6 @@ def test_argument_validation_without_launch(lib):
     # ULTRA activation quantizer needs a level count in [1, 127]
     assert lib.qvit_quantize_act_i8(fake, 4, 16, 16, 2, None, None, None, 0, fake, 16, 16, None) == -1
     # weight packing: npad must be a multiple of the tile
-    assert lib.qvit_pack_weight(fake, 10, 128, 128, 0, fake, fake, None, 4, fake, 100, 128, None, None) == -1
+    assert lib.qvit_pack_weight(fake, 10, 128, 128, 0, fake, fake, None, 4, fake, 128, 128, None, None) == -1
     # zero-size work is a no-op success
     assert lib.qvit_quantize_act_i8(fake, 0, 16, 16, 0, fake, fake, None, 0, fake, 16, 16, None) == 0

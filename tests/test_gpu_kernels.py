@@ -32,7 +32,7 @@ def _round_up(v, m):
 def pack_codes(codes_w: torch.Tensor, wfmt: int, dev):
     """Packs integer weight codes exactly (linear quantizer with d = 1, q_m large => code = w)."""
     n, k = codes_w.shape
-    npad, kpad = _round_up(n, 128), _round_up(k, 128)
+    npad, kpad = _round_up(n, _lib.TILE_N), _round_up(k, _lib.TILE_K)
     w = codes_w.float().to(dev).contiguous()
     ovf = torch.zeros(1, dtype=torch.int32, device=dev)
     packed = _lib.pack_weight(w, _lib.QT_LINEAR, _p(1.0, dev), _p(1000.0, dev), None, wfmt, npad, kpad, ovf)
@@ -144,7 +144,7 @@ def _quant_inputs(g, n=300_000, scale=0.6):
 
 @pytest.mark.parametrize("qt,d,qm,t", [(O.LINEAR, 0.01, 1.0, 1.0), (O.LINEAR, 1 / 127, 1.0, 1.0),
                                        (O.NONLINEAR, 0.01, 1.0, 1.0), (O.NONLINEAR, 0.02, 1.5, 0.9),
-                                       (O.NONLINEAR, 0.005, 0.8, 1.25), (O.LINEAR, 0.05, -0.5, 1.0)])
+                                       (O.NONLINEAR, 0.005, 0.6, 1.25), (O.LINEAR, 0.05, -0.5, 1.0)])
 def test_quantize_act_codes_vs_oracle(dev, qt, d, qm, t):
     g = torch.Generator().manual_seed(3)
     x = _quant_inputs(g)
@@ -164,9 +164,15 @@ def test_quantize_act_codes_vs_oracle(dev, qt, d, qm, t):
     if qt == O.LINEAR:
         assert torch.equal(got, ref)
     else:
-        diff = (got - ref).abs()
+        diff = (got - ref).abs().reshape(-1)
         assert diff.max() <= 1
-        assert (diff > 0).float().mean() <= 1e-4, (diff > 0).float().mean()
+        # random inputs: exp/log are rounded from double on the device, as torch's CPU kernels
+        # are for >99.7% of inputs, so flips need both a non-CR CPU result and a near tie
+        rand_flips = (diff[2000:] > 0).float().mean().item()
+        tie_flips = (diff[1000:2000] > 0).float().mean().item()
+        print(f"nonlinear flips: random {rand_flips:.2e}, crafted ties {tie_flips:.2e}")
+        assert rand_flips <= 1e-5
+        assert tie_flips <= 0.02
 
 
 @pytest.mark.parametrize("qt,t", [(O.LINEAR, 1.0), (O.NONLINEAR, 1.0), (O.NONLINEAR, 0.7)])
@@ -185,10 +191,10 @@ def test_fake_quant_values_vs_oracle(dev, qt, t):
 def test_pack_weight_overflow_flag(dev):
     w = torch.linspace(-1, 1, 128 * 128, device=dev).view(128, 128).contiguous()
     ovf = torch.zeros(1, dtype=torch.int32, device=dev)
-    _lib.pack_weight(w, _lib.QT_LINEAR, _p(1 / 8, dev), _p(1.0, dev), None, _lib.W4, 128, 128, ovf)
+    _lib.pack_weight(w, _lib.QT_LINEAR, _p(1 / 8, dev), _p(1.0, dev), None, _lib.W4, 256, 128, ovf)
     assert ovf.item() == 1          # level 8 does not fit int4
     ovf.zero_()
-    _lib.pack_weight(w, _lib.QT_LINEAR, _p(1 / 7, dev), _p(1.0, dev), None, _lib.W4, 128, 128, ovf)
+    _lib.pack_weight(w, _lib.QT_LINEAR, _p(1 / 7, dev), _p(1.0, dev), None, _lib.W4, 256, 128, ovf)
     assert ovf.item() == 0
 
 

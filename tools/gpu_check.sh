@@ -20,15 +20,15 @@ run() {  # name timeout cmd...
 }
 
 if [[ $STEPS == *tests* ]]; then
-  run pytest_gpu 1200 python -m pytest tests -m gpu -q -rf -p no:cacheprovider ${PYTEST_ARGS:-}
+  run pytest_gpu 600 python -m pytest tests -m gpu -q -rf -p no:cacheprovider ${PYTEST_ARGS:-}
   rc=$?
   if [[ $rc -ge 2 ]]; then echo "pytest crashed/timed out (rc=$rc): stopping"; exit $rc; fi
 fi
 if [[ $STEPS == *bench* ]]; then
-  run bench 900 python bench.py ${BENCH_ARGS:-} || exit $?
+  run bench 360 python bench.py ${BENCH_ARGS:-} || exit $?
 fi
 if [[ $STEPS == *prof* ]]; then
-  run rocprof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline || exit $?
+  run rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline || exit $?
   find "$OUT/prof" -name "*kernel_stats*" -exec cp {} "$OUT/" \; 2>/dev/null
 fi
 echo ALL DONE
