@@ -151,7 +151,7 @@ def main():
             with open(tpath) as f:
                 tj = json.load(f)
             if tj.get("batch") == B and tj.get("model") == args.model:
-                traffic = tj.get("hbm_bytes_per_launch")
+                traffic = tj.get("traffic_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
 

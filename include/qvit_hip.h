@@ -66,6 +66,10 @@ extern "C" {
 #define QVIT_EPI_I8         3  /* C[m,n]  = q_next(d_act d_wt acc + bias[n])        (int8 codes)    */
 #define QVIT_EPI_I32        4  /* C[m,n]  = acc                                      (int32, exact)  */
 
+/* ---- qvit_attention output modes -------------------------------------------------------------- */
+#define QVIT_ATT_F32        0  /* out = softmax(q k^T * scale) v                     (fp32)          */
+#define QVIT_ATT_I8         1  /* out = q_next(softmax(q k^T * scale) v)             (int8 codes)    */
+
 /* Tile geometry the packed operands must be padded to. */
 #define QVIT_TILE_N  256   /* weight rows (out features) are padded to a multiple of this  */
 #define QVIT_TILE_K  128   /* the reduction dim is padded to a multiple of this (zeros)    */
@@ -158,6 +162,24 @@ int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda,
               int epilogue, void* C, int64_t ldc,
               int out_qtype, const float* out_d, const float* out_qm, const float* out_t,
               int out_levels, hipStream_t stream);
+
+/*
+ * Attention core between the qkv and proj QuantizeLinear layers of Attention.forward
+ * (reference vit_model.py:133-149): out = softmax((q @ k^T) * scale) @ v per (image, head),
+ * written as [B*N][ldo] with column h*head_dim + d (the reference's transpose(1, 2).reshape).
+ *   qkv      : fp32 [B*N][ldq], row = [q | k | v], each H*head_dim wide (qkv.reshape(B,N,3,H,hd)).
+ *   head_dim : 64 (the only supported head size); scale: qk_scale (head_dim ** -0.5 by default).
+ *   in_scale : power of two applied to q, k, v before their fp16 hi/lo split (keeps |x * in_scale|
+ *              < 65504; undone exactly), 1.0 for ordinary activations.
+ *   out_mode : QVIT_ATT_F32 -> fp32 out (ldo % 4 == 0, 16-B aligned);
+ *              QVIT_ATT_I8  -> int8 codes of the next layer's activation quantizer
+ *              (out_qtype, out_d, out_qm, out_t, out_levels as in qvit_gemm), ldo % 4 == 0.
+ * fp32 matmuls are formed from fp16 hi/lo products with fp32 accumulation (~2^-22 relative error).
+ */
+int qvit_attention(const float* qkv, int64_t B, int64_t N, int64_t H, int64_t head_dim, int64_t ldq,
+                   float scale, float in_scale, int out_mode, void* out, int64_t ldo,
+                   int out_qtype, const float* out_d, const float* out_qm, const float* out_t,
+                   int out_levels, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -31,6 +31,9 @@ EPI_I8_GELU = 2
 EPI_I8 = 3
 EPI_I32 = 4
 
+ATT_F32 = 0
+ATT_I8 = 1
+
 TILE_N = 256
 TILE_K = 128
 
@@ -51,6 +54,8 @@ _SIGNATURES = {
                                 _c_p, _i64, _i64, _c_p],
     "qvit_gemm": [_c_p, _i64, _i64, _i64, _c_p, _i32, _i64, _i64, _c_p, _c_p, _c_p, _i32, _c_p, _i64,
                   _i32, _c_p, _c_p, _c_p, _i32, _c_p],
+    "qvit_attention": [_c_p, _i64, _i64, _i64, _i64, _i64, _f32, _f32, _i32, _c_p, _i64, _i32, _c_p, _c_p, _c_p,
+                       _i32, _c_p],
 }
 STRING_FUNCS = {"qvit_strerror": [_i32], "qvit_version": []}
 EXPORTED_SYMBOLS = sorted(list(_SIGNATURES) + list(STRING_FUNCS))
@@ -182,3 +187,15 @@ def gemm(A: torch.Tensor, M: int, K: int, packed: torch.Tensor, wfmt: int, N: in
                             _ptr(bias_pad), epilogue, _ptr(C), C.stride(0), out_qtype, _ptr(out_d), _ptr(out_qm),
                             _ptr(out_t), out_levels, _stream(A.device)), "qvit_gemm")
     return C
+
+
+def attention(qkv: torch.Tensor, B: int, N: int, H: int, head_dim: int, scale: float, out: torch.Tensor,
+              out_mode: int = ATT_F32, in_scale: float = 1.0, out_qtype: int = 0, out_d=None, out_qm=None,
+              out_t=None, out_levels: int = 0) -> torch.Tensor:
+    """softmax(q k^T * scale) v per (image, head) on a [B*N, >= 3*H*hd] fp32 qkv projection."""
+    _require_gpu(qkv, "qkv")
+    assert qkv.dtype == torch.float32 and qkv.stride(1) == 1
+    _check(load().qvit_attention(_ptr(qkv), B, N, H, head_dim, qkv.stride(0), scale, in_scale, out_mode, _ptr(out),
+                                 out.stride(0), out_qtype, _ptr(out_d), _ptr(out_qm), _ptr(out_t), out_levels,
+                                 _stream(qkv.device)), "qvit_attention")
+    return out

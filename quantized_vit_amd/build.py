@@ -19,7 +19,7 @@ BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libqvit_hip.so")
 ARCH = "gfx950"
 
-SOURCES = ["quant_kernels.hip", "gemm_w4a8.hip"]
+SOURCES = ["quant_kernels.hip", "gemm_w4a8.hip", "attention.hip"]
 HEADERS = ["qvit_common.h"]
 
 HIPCC_FLAGS = [
@@ -49,19 +49,23 @@ def _newest_input_mtime() -> float:
     return max(os.path.getmtime(p) for p in paths)
 
 
-def is_stale() -> bool:
-    return not os.path.exists(LIB) or os.path.getmtime(LIB) < _newest_input_mtime()
+def is_stale(lib: str = LIB) -> bool:
+    return not os.path.exists(lib) or os.path.getmtime(lib) < _newest_input_mtime()
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not is_stale():
-        return LIB
+def build(force: bool = False, verbose: bool = False, defines: tuple = (), lib: str = LIB,
+          build_dir: str = BUILD) -> str:
+    """Builds the library. `defines`/`lib`/`build_dir` produce diagnostic variants (e.g. the
+    QVIT_GEMM_STAMPS phase-timing build used by tools/gemm_stamps.py) without touching LIB."""
+    if not force and not is_stale(lib):
+        return lib
     hipcc = _hipcc()
-    os.makedirs(BUILD, exist_ok=True)
+    os.makedirs(build_dir, exist_ok=True)
+    dflags = [f"-D{d}" for d in defines]
 
     def compile_one(src: str) -> str:
-        obj = os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
-        cmd = [hipcc, *HIPCC_FLAGS, "-I", INCLUDE, "-c", os.path.join(CSRC, src), "-o", obj]
+        obj = os.path.join(build_dir, os.path.splitext(src)[0] + ".o")
+        cmd = [hipcc, *HIPCC_FLAGS, *dflags, "-I", INCLUDE, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         res = subprocess.run(cmd, capture_output=True, text=True)
@@ -73,13 +77,13 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
     with ThreadPoolExecutor(max_workers=min(4, len(SOURCES))) as ex:
         objs = list(ex.map(compile_one, SOURCES))
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"link failed:\n{res.stdout}\n{res.stderr}")
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib)
+    return lib
 
 
 def main() -> None:

@@ -104,6 +104,36 @@ struct EpiArgs {
   int out_levels;
 };
 
+// Diagnostic build only (-DQVIT_GEMM_STAMPS, tools/gemm_stamps.py): per-phase s_memtime cycle sums.
+// In the product library these macros are empty.
+#ifdef QVIT_GEMM_STAMPS
+__device__ unsigned long long qvit_gemm_stamp_sums[8];
+#define QVIT_STAMP_DECL                                 \
+  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0};   \
+  unsigned long long st_prev = __builtin_amdgcn_s_memtime();
+#define QVIT_STAMP(i)                                          \
+  do {                                                         \
+    const unsigned long long st_t = __builtin_amdgcn_s_memtime(); \
+    st_acc[i] += st_t - st_prev;                               \
+    st_prev = st_t;                                            \
+  } while (0)
+#define QVIT_STAMP_FLUSH                                                   \
+  do {                                                                     \
+    if (lane == 0) {                                                       \
+      for (int st_i = 0; st_i < 6; ++st_i) atomicAdd(&qvit_gemm_stamp_sums[st_i], st_acc[st_i]); \
+      atomicAdd(&qvit_gemm_stamp_sums[7], 1ull);                           \
+    }                                                                      \
+  } while (0)
+#else
+#define QVIT_STAMP_DECL
+#define QVIT_STAMP(i) \
+  do {                \
+  } while (0)
+#define QVIT_STAMP_FLUSH \
+  do {                   \
+  } while (0)
+#endif
+
 template <int WFMT>
 struct Frags {
   v4i x[8];
@@ -146,6 +176,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   // epilogue scalars are loaded before the main loop: no compiler VMEM op lands among the DMAs
   float alpha = 0.f;
   if (EPI != QVIT_EPI_I32) alpha = (*ep.d_act) * (*ep.d_wt);
+  QVIT_STAMP_DECL
 
   // ---- LDS-DMA sources (per lane) and destinations (per wave) ---------------------------------
   // activations: wave w stages rows [32w, 32w+32) as 2 pieces of 16 rows x 64 B
@@ -153,7 +184,11 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
 #pragma unroll
   for (int j = 0; j < G::XPIECES; ++j) {
     const int row = 32 * wave + 16 * j + (lane >> 2);
+#if defined(QVIT_GEMM_ABL)
+    int gm = (QVIT_GEMM_ABL == 5 ? 0 : m0) + row;
+#else
     int gm = m0 + row;
+#endif
     gm = gm < M ? gm : M - 1;  // clamp the tail: staged, never stored
     const int logical = (lane & 3) ^ (((row >> 2) & 1) << 1);
     xsrc[j] = A + (int64_t)gm * lda + logical * 16;
@@ -173,13 +208,32 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
       row = WROWS_PER_WAVE * wave + WROWS_PER_PIECE * j + (lane >> 2);
       logical = (lane & 3) ^ (((row >> 2) & 1) << 1);
     }
+#if defined(QVIT_GEMM_ABL)
+    wsrc[j] = Wp + (int64_t)((QVIT_GEMM_ABL == 5 ? 0 : n0) + row) * wrow_bytes + logical * 16;
+#else
     wsrc[j] = Wp + (int64_t)(n0 + row) * wrow_bytes + logical * 16;
+#endif
   }
   const uint32_t lds0 = lds_addr(smem);
 
   auto issue_stage = [&](int kt) {
     const uint32_t sx = lds0 + (uint32_t)((kt % RING) * G::STAGE);
     const uint32_t sw = sx + XBYTES;
+#if defined(QVIT_GEMM_ABL)  // diagnostic builds only (tools/gemm_stamps.py --abl): wrong results
+    if (QVIT_GEMM_ABL == 1) return;  // no DMA
+    if (QVIT_GEMM_ABL == 4) {        // contiguous 1-KiB pieces from a 128 KiB L2-hot window
+      const int8_t* bx = A + (kt % 8) * 16384 + wave * 2048 + lane * 16;
+      const int8_t* bw = Wp + (kt % 8) * 8192 + wave * G::WPIECES * 1024 + lane * 16;
+#pragma unroll
+      for (int j = 0; j < G::XPIECES; ++j)
+        dma16(bx + j * 1024, __builtin_amdgcn_readfirstlane(sx + (32 * wave + 16 * j) * BK));
+#pragma unroll
+      for (int j = 0; j < G::WPIECES; ++j)
+        dma16(bw + j * 1024,
+              __builtin_amdgcn_readfirstlane(sw + (WROWS_PER_WAVE * wave + WROWS_PER_PIECE * j) * G::WROW));
+      return;
+    }
+#endif
     const int64_t kx = (int64_t)kt * BK;
     const int64_t kw = (WFMT == QVIT_W4) ? kx / 2 : kx;
 #pragma unroll
@@ -245,15 +299,19 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     // sched_barrier(0) fences keep the phases in this order: the steady loop is one basic block and
     // the scheduler otherwise hoists nxt's unpack up to its reads (forcing a wait) across steps.
     __builtin_amdgcn_s_waitcnt(0xC07F);
+    QVIT_STAMP(5);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (decltype(issue)::value) issue_stage(kt + AHEAD);
+    QVIT_STAMP(1);
     if constexpr (decltype(read)::value) {
       stage_sync<decltype(sync)::value>();
+      QVIT_STAMP(2);
       read_frags(kt + 1, nxt);
     }
     __builtin_amdgcn_sched_barrier(0);
     mfma_stage(cur);
     __builtin_amdgcn_sched_barrier(0);
+    QVIT_STAMP(3);
   };
   using Yes = std::true_type;
   using No = std::false_type;
@@ -268,6 +326,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   if (nk > 2) stage_sync<2 * D>();
   else stage_sync<D>();
   read_frags(0, fa);
+  QVIT_STAMP(0);
   int kt = 0;
   if constexpr (!SHORT)
   for (; kt + 5 <= nk; kt += 2) {  // both steps issue, two newer stages in flight
@@ -367,6 +426,8 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     }
     __syncthreads();
   }
+  QVIT_STAMP(4);
+  QVIT_STAMP_FLUSH;
 }
 
 template <int WFMT, int EPI>
@@ -426,3 +487,15 @@ extern "C" int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda, con
   if (wfmt == QVIT_W4) return dispatch_epi<QVIT_W4>(epilogue, A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
   return dispatch_epi<QVIT_W8>(epilogue, A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
 }
+
+#ifdef QVIT_GEMM_STAMPS
+// Diagnostic entry points (not part of include/qvit_hip.h): phase sums
+// [0 prologue, 1 DMA issue, 2 stage wait, 3 fragment reads + MFMA issue, 4 epilogue, 5 step-top drain, 7 waves].
+extern "C" int qvit_gemm_stamps(unsigned long long* host8, int reset) {
+  if (reset) {
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    return qvit_hip_status(hipMemcpyToSymbol(HIP_SYMBOL(qvit_gemm_stamp_sums), z, sizeof(z)));
+  }
+  return qvit_hip_status(hipMemcpyFromSymbol(host8, HIP_SYMBOL(qvit_gemm_stamp_sums), 8 * sizeof(unsigned long long)));
+}
+#endif

@@ -250,9 +250,12 @@ class QuantizeMixin:
         qm_act = _as_param_ptr(getattr(self, "q_m_act", None), dev) if wa else None
         t_act = _as_param_ptr(getattr(self, "t_quant_act", None), dev) if wa else None
         # one host sync: the scalar parameters decide the storage format
+        bias_max = (self.bias.detach().abs().max().float().reshape(1).to(dev) if self.bias is not None
+                    else torch.zeros(1, device=dev))
         scal = torch.stack([x.reshape(-1)[0] for x in (d_wt, qm_wt, t_wt if t_wt is not None else d_wt)]
                            + ([d_act.reshape(-1)[0], qm_act.reshape(-1)[0],
-                               (t_act if t_act is not None else d_act).reshape(-1)[0]] if wa else [])).cpu()
+                               (t_act if t_act is not None else d_act).reshape(-1)[0]] if wa else [])
+                           + [bias_max[0]]).cpu()
         s = scal.tolist()
         lw = saturation_level(qt, s[0], s[1], s[2] if t_wt is not None else 1.0)
         la = saturation_level(qt, s[3], s[4], s[5] if t_act is not None else 1.0) if wa else float("inf")
@@ -272,6 +275,8 @@ class QuantizeMixin:
         if plan.int_path:
             bias = self.bias.detach() if self.bias is not None else None
             plan.bias_pad = _lib.pad_bias(bias, n, npad, dev)
+            # |output| <= d_act d_wt sum_k |a_k||w_k| + |bias| <= d_act d_wt K L_a L_w + max|bias|
+            plan.extra["out_bound"] = abs(s[3] * s[0]) * k * abs(la) * abs(lw) + s[-1]
         else:
             wq = _lib.fake_quant_f32(self.weight.detach().float(), qt, d_wt, qm_wt, t_wt)
             plan.w_fakequant = wq

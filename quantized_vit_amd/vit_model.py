@@ -19,6 +19,8 @@ from collections import OrderedDict
 from functools import partial
 from typing import Optional
 
+import math
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -95,8 +97,27 @@ class ViTAttention(nn.Module):
         self.proj = nn.Linear(dim, dim)
         self.proj_drop = nn.Dropout(proj_drop_ratio)
 
+    def hip_ok(self, qkv: torch.Tensor) -> bool:
+        return (qkv.is_cuda and qkv.dtype == torch.float32 and self.head_dim == 64 and qkv.dim() == 2
+                and qkv.stride(1) == 1 and not (self.training and self.attn_drop.p > 0))
+
+    def core_hip(self, qkv: torch.Tensor, B: int, N: int, out: torch.Tensor, out_mode: int = _lib.ATT_F32,
+                 in_scale: float = 1.0, plan=None) -> torch.Tensor:
+        """The same op on the fused HIP kernel (qvit_attention); with out_mode ATT_I8 it also applies the
+        activation quantizer of `plan` (the proj layer) and writes its int8 codes."""
+        if out_mode == _lib.ATT_I8:
+            return _lib.attention(qkv, B, N, self.num_heads, 64, self.scale, out, out_mode, in_scale, plan.qtype,
+                                  plan.d_act, plan.qm_act, plan.t_act)
+        return _lib.attention(qkv, B, N, self.num_heads, 64, self.scale, out, out_mode, in_scale)
+
     def core(self, qkv: torch.Tensor, B: int, N: int) -> torch.Tensor:
         """softmax(q k^T * scale) v on the qkv projection (vit_model.py:133-149), fp32."""
+        if self.hip_ok(qkv.reshape(B * N, -1)):
+            q2 = qkv.reshape(B * N, -1)
+            out = torch.empty((B * N, self.num_heads * 64), dtype=torch.float32, device=qkv.device)
+            amax = float(q2.abs().max()) if q2.numel() else 0.0   # unfused path: no plan bound, one sync
+            scale = 1.0 if amax <= 16384.0 else 2.0 ** -math.ceil(math.log2(amax / 16384.0))
+            return self.core_hip(q2, B, N, out, _lib.ATT_F32, scale).reshape(B, N, -1)
         qkv = qkv.reshape(B, N, 3, self.num_heads, -1).permute(2, 0, 3, 1, 4)
         q, k, v = qkv[0], qkv[1], qkv[2]
         attn = (q @ k.transpose(-2, -1)) * self.scale
@@ -131,6 +152,17 @@ class Mlp(nn.Module):
         x = self.fc2(x)
         x = self.drop(x)
         return x
+
+
+def attention_in_scale(p_qkv) -> float:
+    """Power of two that keeps the qkv projection (|x| <= its plan's output bound) inside the fp16
+    range of the attention kernel's hi/lo split (qvit_attention's in_scale)."""
+    bound = p_qkv.extra.get("out_bound", float("inf"))
+    if bound <= 16384.0:
+        return 1.0
+    if not math.isfinite(bound):
+        raise _lib.QvitError("qkv projection has no finite output bound; cannot size the attention input scale")
+    return 2.0 ** -math.ceil(math.log2(bound / 16384.0))
 
 
 def _qlinear_int(m: nn.Module) -> bool:
@@ -192,9 +224,16 @@ class Block(nn.Module):
         qkv = a.qkv.gemm_codes(codes, p_qkv, _lib.EPI_F32)
         if qkv.shape[1] != p_qkv.n:
             qkv = qkv[:, :p_qkv.n]
-        h = a.core(qkv, B, N).reshape(M, -1)
         p_proj = a.proj.quant_plan()
-        codes = a.proj._act_codes(h if h.is_contiguous() else h.contiguous(), p_proj)
+        if a.hip_ok(qkv):
+            # attention core + proj's activation quantizer in one kernel: int8 codes for the proj GEMM
+            codes = torch.empty((M, p_proj.kpad), dtype=torch.int8, device=x.device)
+            if p_proj.kpad != a.num_heads * 64:
+                codes[:, a.num_heads * 64:].zero_()
+            a.core_hip(qkv, B, N, codes, _lib.ATT_I8, attention_in_scale(p_qkv), p_proj)
+        else:
+            h = a.core(qkv, B, N).reshape(M, -1)
+            codes = a.proj._act_codes(h if h.is_contiguous() else h.contiguous(), p_proj)
         a.proj.gemm_codes(codes, p_proj, _lib.EPI_F32_RESID, out=x2)
         # x + mlp(norm2(x))
         p_fc1 = m.fc1.quant_plan()

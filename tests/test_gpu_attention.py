@@ -1,0 +1,112 @@
+"""GPU parity of qvit_attention (Attention.forward's core, reference vit_model.py:133-149).
+
+Reference: the same softmax(q k^T * scale) v evaluated in fp64 on the CPU from the same fp32 qkv.
+Bars: fp32 output within 2e-6 of max|out| for ordinary logits; 1e-5 for near one-hot rows with logits of
+std ~36 (the fp16 hi/lo split carries each operand to 22 bits, so a logit's absolute error grows with
+sum |q_i k_i|, and a softmax row turns it into the same relative error on the output); int8-code output
+equal to the oracle's quantizer applied to the fp64 result except at rounding ties (<= 1e-3 of codes,
+each off by one).
+"""
+import math
+
+import pytest
+import torch
+
+from oracle import quant_oracle as O
+from quantized_vit_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+
+def _p(v, dev):
+    return torch.tensor([float(v)], dtype=torch.float32, device=dev)
+
+
+def ref_attention(qkv: torch.Tensor, B: int, N: int, H: int, hd: int, scale: float) -> torch.Tensor:
+    """vit_model.py:133-149 in fp64."""
+    x = qkv[:, :3 * H * hd].double().reshape(B, N, 3, H, hd).permute(2, 0, 3, 1, 4)
+    q, k, v = x[0], x[1], x[2]
+    a = ((q @ k.transpose(-2, -1)) * scale).softmax(dim=-1)
+    return (a @ v).transpose(1, 2).reshape(B * N, H * hd)
+
+
+def run(dev, B, N, H, qkv, scale, mode=_lib.ATT_F32, in_scale=1.0, **qkw):
+    if mode == _lib.ATT_F32:
+        out = torch.full((B * N, H * 64), float("nan"), device=dev)
+    else:
+        out = torch.zeros((B * N, H * 64), dtype=torch.int8, device=dev)
+    _lib.attention(qkv.to(dev), B, N, H, 64, scale, out, mode, in_scale, **qkw)
+    torch.cuda.synchronize()
+    return out.cpu()
+
+
+@pytest.mark.parametrize("B,N,H", [(2, 197, 12), (1, 1, 1), (3, 33, 2), (1, 64, 3), (2, 577, 2), (1, 300, 1)])
+def test_attention_fp32_vs_fp64(dev, B, N, H):
+    g = torch.Generator().manual_seed(N * 7 + H)
+    qkv = torch.randn(B * N, 3 * H * 64, generator=g) * 1.5
+    scale = 64 ** -0.5
+    ref = ref_attention(qkv, B, N, H, 64, scale)
+    out = run(dev, B, N, H, qkv, scale)
+    assert torch.isfinite(out).all()
+    err = (out.double() - ref).abs().max().item()
+    assert err <= 2e-6 * ref.abs().max().item(), err
+
+
+def test_attention_row_stride_and_peaked_softmax(dev):
+    """ldq wider than 3*H*hd (qkv sliced from a padded GEMM output) and near one-hot softmax rows."""
+    B, N, H = 2, 197, 4
+    g = torch.Generator().manual_seed(5)
+    full = torch.randn(B * N, 3 * H * 64 + 64, generator=g) * 6.0
+    qkv = full[:, :3 * H * 64]
+    ref = ref_attention(qkv, B, N, H, 64, 0.125)
+    out = torch.empty((B * N, H * 64), device=dev)
+    _lib.attention(full.to(dev)[:, :3 * H * 64], B, N, H, 64, 0.125, out)
+    torch.cuda.synchronize()
+    err = (out.cpu().double() - ref).abs().max().item()
+    assert err <= 1e-5 * ref.abs().max().item(), err
+
+
+def test_attention_in_scale_large_inputs(dev):
+    """|q|, |k|, |v| beyond the fp16 range: a power-of-two in_scale keeps the split exact."""
+    B, N, H = 1, 100, 2
+    g = torch.Generator().manual_seed(9)
+    qkv = torch.randn(B * N, 3 * H * 64, generator=g)
+    qkv[:, 2 * H * 64:] *= 2.0e5           # v beyond 65504
+    qkv[:, :2 * H * 64] *= 1.5             # ordinary logits: this test isolates the scaling
+    ref = ref_attention(qkv, B, N, H, 64, 0.125)
+    out = run(dev, B, N, H, qkv, 0.125, in_scale=2.0 ** -5)   # |v| <= ~1e6 -> < 65504 after scaling
+    err = (out.double() - ref).abs().max().item()
+    assert err <= 2e-6 * ref.abs().max().item(), err
+
+
+@pytest.mark.parametrize("qt,t", [(O.LINEAR, 1.0), (O.NONLINEAR, 1.0), (O.NONLINEAR, 0.8)])
+def test_attention_int8_codes_vs_oracle(dev, qt, t):
+    B, N, H = 2, 197, 12
+    g = torch.Generator().manual_seed(11)
+    qkv = torch.randn(B * N, 3 * H * 64, generator=g)
+    ref = ref_attention(qkv, B, N, H, 64, 0.125)
+    d, qm = 1.2 / 127, 1.2
+    if qt == O.NONLINEAR:
+        d = qm ** t / 127
+    want = O.quant_codes(ref.float(), qt, d, qm, t if qt == O.NONLINEAR else None).to(torch.int32)
+    qtc = _lib.QT_LINEAR if qt == O.LINEAR else _lib.QT_NONLINEAR
+    got = run(dev, B, N, H, qkv, 0.125, mode=_lib.ATT_I8, out_qtype=qtc, out_d=_p(d, dev), out_qm=_p(qm, dev),
+              out_t=_p(t, dev) if qt == O.NONLINEAR else None).to(torch.int32)
+    diff = (got - want).abs()
+    assert diff.max().item() <= 1
+    assert (diff > 0).float().mean().item() <= 1e-3
+
+
+def test_attention_argument_validation(dev):
+    qkv = torch.zeros(10, 3 * 64, device=dev)
+    out = torch.zeros(10, 64, device=dev)
+    lib = _lib.load()
+    s = torch.cuda.current_stream().cuda_stream
+    assert lib.qvit_attention(qkv.data_ptr(), 1, 10, 1, 32, 192, 0.125, 1.0, 0, out.data_ptr(), 64, 0, None, None,
+                              None, 0, s) == -1            # head_dim != 64
+    assert lib.qvit_attention(qkv.data_ptr(), 1, 10, 1, 64, 100, 0.125, 1.0, 0, out.data_ptr(), 64, 0, None, None,
+                              None, 0, s) == -1            # ldq < 3 H hd
+    assert lib.qvit_attention(qkv.data_ptr(), 1, 10, 1, 64, 192, 0.125, 1.0, 1, out.data_ptr(), 64, 1, None, None,
+                              None, 0, s) == -1            # int8 mode without quantizer params
+    assert lib.qvit_attention(qkv.data_ptr(), 1, 10, 1, 64, 192, 0.125, 0.0, 0, out.data_ptr(), 64, 0, None, None,
+                              None, 0, s) == -1            # in_scale must be > 0

@@ -150,7 +150,9 @@ def check_vit_parity(model, cfg, img, dev, block_tol=1e-3, floor_factor=2.5):
 
     1. Teacher-forced: the patch embedding, every block and the head are run on the GPU on the
        ORACLE's input to that stage; each output must match the oracle's within block_tol
-       (north-star tolerance, applied per stage).
+       (north-star tolerance, applied per stage), or, for a block, within floor_factor x that
+       block's own fp64-vs-fp32 distance on the same input (a block whose quantizers sit on many
+       near-ties differs from itself by more than 1e-3 between fp32 and fp64).
     2. End-to-end: quantizers turn ulp-level arithmetic differences into code flips that compound
        over the blocks, so the reference's own fp32 forward differs from the same op sequence in
        fp64 by ~1e-2 (measured here as `floor`). The GPU logits must be as close to the fp32
@@ -164,10 +166,13 @@ def check_vit_parity(model, cfg, img, dev, block_tol=1e-3, floor_factor=2.5):
         x = model.patch_embed(img.to(dev))
         x = torch.cat((model.cls_token.expand(x.shape[0], -1, -1), x), dim=1) + model.pos_embed
         errs = {"embed": rel(x, trace[0])}
+        tols = {}
         for i, blk in enumerate(model.blocks):
             assert blk.fused_ok(x)
             out = blk.forward_fused_(trace[i].to(dev).contiguous().clone())
             errs[f"block{i}"] = rel(out, trace[i + 1])
+            stage_floor = rel(O.vit_block(trace[i].double(), sd64, cfg, i), trace[i + 1])
+            tols[f"block{i}"] = max(block_tol, floor_factor * stage_floor)
         head = model.head(model.norm(trace[-1].to(dev))[:, 0])
         errs["head"] = rel(head, ref32)
         y = model(img.to(dev))
@@ -176,7 +181,8 @@ def check_vit_parity(model, cfg, img, dev, block_tol=1e-3, floor_factor=2.5):
     worst = max(errs.values())
     print(f"teacher-forced worst stage {worst:.2e} ({max(errs, key=errs.get)}); end-to-end gpu-vs-fp32 {r:.3e}, "
           f"reference fp64-vs-fp32 floor {floor:.3e}")
-    assert worst < block_tol, errs
+    bad = {k: (e, tols.get(k, block_tol)) for k, e in errs.items() if e >= tols.get(k, block_tol)}
+    assert not bad, bad
     assert r <= floor_factor * floor + 1e-4, (r, floor)
     return errs, r, floor
 
@@ -219,9 +225,108 @@ def test_vit_fused_equals_modulewise(dev):
     assert rel(fused, ref) < 1e-4
 
 
+def stage_forced_block(model, cfg, sd, x, i, dev):
+    """Block i with the ORACLE's values entering every kernel (quantizer-boundary forcing): each stage
+    of the fused block is compared in isolation, so one tie flip cannot cascade through attention.
+    Returns {stage: (kind, metric)}: codes -> fraction of differing codes (and max |diff|), fp32 -> rel."""
+    blk = model.blocks[i]
+    pre = f"blocks.{i}"
+    B, N, C = x.shape
+    M = B * N
+    res = {}
+
+    def ocodes(v, name):
+        q = O.LayerQ.from_state(sd, f"{pre}.{name}.", cfg.quant_type, cfg.quant_mode)
+        return O.quant_codes(v.reshape(M, -1), q.quant_type, q.d_act, q.q_m_act, q.t_act)
+
+    def cmp_codes(name, got, want):
+        d = (got.cpu().to(torch.int32) - want.to(torch.int32)).abs()
+        res[name] = ("codes", (d > 0).float().mean().item(), d.max().item())
+
+    def gemm_ref(name, layer, a_codes):
+        """fp64 d_a d_w (A . W^T) + b on the GPU's own weight codes; their tie-level differences from the
+        oracle's weight codes are checked as a quantizer stage of their own."""
+        q = O.LayerQ.from_state(sd, f"{pre}.{name}.", cfg.quant_type, cfg.quant_mode)
+        pl = layer.quant_plan()
+        w = layer.weight.detach().float().contiguous()
+        wg = (_lib.fake_quant_f32(w, pl.qtype, pl.d_wt, pl.qm_wt, pl.t_wt).cpu().double() / q.d_wt).round()
+        cmp_codes(name + " weight codes", wg, O.quant_codes(w.cpu(), q.quant_type, q.d_wt, q.q_m_wt, q.t_wt))
+        out = q.d_act * q.d_wt * (a_codes.double() @ wg.t())
+        return out + layer.bias.detach().cpu().double() if layer.bias is not None else out
+
+    h1 = O._layer_norm(x, sd, pre + ".norm1")
+    qkv = O._qlin(h1, sd, pre + ".attn.qkv", cfg)
+    q_, k_, v_ = qkv.reshape(B, N, 3, -1, cfg.hd()).permute(2, 0, 3, 1, 4)
+    ao = (((q_ @ k_.transpose(-2, -1)) * cfg.hd() ** -0.5).softmax(-1) @ v_).transpose(1, 2).reshape(B, N, -1)
+    x1 = x + O._qlin(ao, sd, pre + ".attn.proj", cfg)
+    h2 = O._layer_norm(x1, sd, pre + ".norm2")
+    g1 = F.gelu(O._qlin(h2, sd, pre + ".mlp.fc1", cfg))
+    x2 = x1 + O._qlin(g1, sd, pre + ".mlp.fc2", cfg)
+
+    pq, pp, p1, p2 = (blk.attn.qkv.quant_plan(), blk.attn.proj.quant_plan(), blk.mlp.fc1.quant_plan(),
+                      blk.mlp.fc2.quant_plan())
+    c = torch.empty((M, pq.kpad), dtype=torch.int8, device=dev)
+    _lib.layernorm_quant_i8(x.to(dev).reshape(M, C).contiguous(), blk.norm1.weight, blk.norm1.bias, blk.norm1.eps,
+                            pq.qtype, pq.d_act, pq.qm_act, pq.t_act, 0, c, pq.kpad)
+    cmp_codes("norm1 codes", c[:, :C], ocodes(h1, "attn.qkv"))
+    want_c = ocodes(h1, "attn.qkv").to(torch.int8)
+    c = torch.zeros((M, pq.kpad), dtype=torch.int8, device=dev)
+    c[:, :C] = want_c.to(dev)
+    g_qkv = blk.attn.qkv.gemm_codes(c, pq, _lib.EPI_F32)[:, :pq.n]
+    res["qkv"] = ("fp32", rel(g_qkv, gemm_ref("attn.qkv", blk.attn.qkv, want_c)))
+    ca = torch.zeros((M, pp.kpad), dtype=torch.int8, device=dev)
+    blk.attn.core_hip(qkv.reshape(M, -1).to(dev).contiguous(), B, N, ca, _lib.ATT_I8, 1.0, pp)
+    cmp_codes("attention codes", ca[:, :C], ocodes(ao, "attn.proj"))
+    ca = torch.zeros((M, pp.kpad), dtype=torch.int8, device=dev)
+    want_a = ocodes(ao, "attn.proj").to(torch.int8)
+    ca[:, :C] = want_a.to(dev)
+    xr = x.to(dev).reshape(M, C).contiguous().clone()
+    blk.attn.proj.gemm_codes(ca, pp, _lib.EPI_F32_RESID, out=xr)
+    res["x + proj"] = ("fp32", rel(xr, x.reshape(M, C).double() + gemm_ref("attn.proj", blk.attn.proj, want_a)))
+    c2 = torch.empty((M, p1.kpad), dtype=torch.int8, device=dev)
+    _lib.layernorm_quant_i8(x1.to(dev).reshape(M, C).contiguous(), blk.norm2.weight, blk.norm2.bias,
+                            blk.norm2.eps, p1.qtype, p1.d_act, p1.qm_act, p1.t_act, 0, c2, p1.kpad)
+    cmp_codes("norm2 codes", c2[:, :C], ocodes(h2, "mlp.fc1"))
+    c2 = torch.zeros((M, p1.kpad), dtype=torch.int8, device=dev)
+    c2[:, :C] = ocodes(h2, "mlp.fc1").to(torch.int8).to(dev)
+    hid = torch.zeros((M, p2.kpad), dtype=torch.int8, device=dev)
+    blk.mlp.fc1.gemm_codes(c2, p1, _lib.EPI_I8_GELU, out=hid, next_layer=blk.mlp.fc2)
+    cmp_codes("fc1+gelu codes", hid[:, :p1.n], ocodes(g1, "mlp.fc2"))
+    hid = torch.zeros((M, p2.kpad), dtype=torch.int8, device=dev)
+    want_g = ocodes(g1, "mlp.fc2").to(torch.int8)
+    hid[:, :p1.n] = want_g.to(dev)
+    xr2 = x1.to(dev).reshape(M, C).contiguous().clone()
+    blk.mlp.fc2.gemm_codes(hid, p2, _lib.EPI_F32_RESID, out=xr2)
+    res["x1 + fc2"] = ("fp32", rel(xr2, x1.reshape(M, C).double() + gemm_ref("mlp.fc2", blk.mlp.fc2, want_g)))
+    gemm_ref("mlp.fc1", blk.mlp.fc1, c2[:, :C].cpu())   # records fc1's weight-code stage
+    return res
+
+
 def test_vit_base_b2_vs_oracle(dev):
+    """ViT-B: a single rounding-tie code flip entering attention moves a whole block's output by
+    ~3e-3 (measured: 1 LayerNorm code in 302K), so block-level teacher forcing cannot hold 1e-3 here.
+    Parity is pinned stage by stage instead (every kernel of every block on the oracle's input: fp32
+    stages within 1e-6 of an fp64 product of the same codes, activation codes identical except ties
+    (<= 1e-4 of them, off by one), weight codes identical except ties (<= 1e-5; the CPU's fp32
+    exp(t log|w|) is not correctly rounded, the GPU's is)), plus the end-to-end logits against the
+    fp64-vs-fp32 floor."""
     model = build_quantized_vit("vit_base_patch16_224", seed=0).to(dev)
-    check_vit_parity(model, O.ViTConfig(), synthetic_images(2, 224, seed=5), dev)
+    cfg = O.ViTConfig()
+    img = synthetic_images(2, 224, seed=5)
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    trace = []
+    with torch.no_grad():
+        ref32 = O.vit_forward(sd, cfg, img, trace=trace)
+        ref64 = O.vit_forward({k: v.double() for k, v in sd.items()}, cfg, img.double())
+        for i in range(cfg.depth):
+            for name, r in stage_forced_block(model, cfg, sd, trace[i], i, dev).items():
+                if r[0] == "fp32":
+                    assert r[1] <= 1e-6, (i, name, r)
+                else:   # activation codes: ties <= 1e-4; weight codes: ties <= 1e-5
+                    assert r[1] <= (1e-5 if "weight" in name else 1e-4) and r[2] <= 1, (i, name, r)
+        y = model(img.to(dev))
+    floor = rel(ref64, ref32)
+    assert rel(y, ref32) <= 2.5 * floor + 1e-4, (rel(y, ref32), floor)
 
 
 def test_pruned_shapes_vs_oracle(dev):

@@ -1,0 +1,57 @@
+"""Times qvit_attention on the ViT-B/16 b256 shape (B=256, N=197, H=12, hd=64) against torch's fp32
+bmm + softmax + bmm sequence on the same qkv, with HIP events (median over iters)."""
+import argparse
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from quantized_vit_amd import _lib  # noqa: E402
+
+
+def timeit(fn, iters):
+    ts = []
+    for _ in range(iters + 2):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        ts.append((s, e))
+    torch.cuda.synchronize()
+    ms = sorted(s.elapsed_time(e) for s, e in ts[2:])
+    return ms[len(ms) // 2]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--B", type=int, default=256)
+    ap.add_argument("--N", type=int, default=197)
+    ap.add_argument("--H", type=int, default=12)
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    B, N, H = a.B, a.N, a.H
+    qkv = torch.randn(B * N, 3 * H * 64, device=dev)
+    out = torch.empty(B * N, H * 64, device=dev)
+    codes = torch.empty(B * N, H * 64, dtype=torch.int8, device=dev)
+    d, qm = torch.tensor([2.0 / 127], device=dev), torch.tensor([2.0], device=dev)
+    t = torch.tensor([1.0], device=dev)
+
+    def torch_ref():
+        x = qkv.reshape(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+        at = ((x[0] @ x[1].transpose(-2, -1)) * 0.125).softmax(dim=-1)
+        return (at @ x[2]).transpose(1, 2).reshape(B * N, H * 64)
+
+    f32 = timeit(lambda: _lib.attention(qkv, B, N, H, 64, 0.125, out), a.iters)
+    i8 = timeit(lambda: _lib.attention(qkv, B, N, H, 64, 0.125, codes, _lib.ATT_I8, 1.0, _lib.QT_NONLINEAR, d, qm, t),
+                a.iters)
+    tr = timeit(torch_ref, a.iters)
+    flops = 4.0 * B * H * N * N * 64
+    for name, ms in (("qvit_attention f32", f32), ("qvit_attention i8", i8), ("torch fp32", tr)):
+        print(f"{name:20s} {ms*1e3:9.1f} us  {flops/ms/1e9:8.1f} TFLOP/s (fp32-equivalent)", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,78 @@
+"""Where a GEMM wave's cycles go: runs the GEMM microbenchmark shapes on a diagnostic build of the
+library (-DQVIT_GEMM_STAMPS: s_memtime stamps around each pipeline phase, summed over waves) and
+prints the per-wave phase breakdown in shader cycles.
+
+    python tools/gemm_stamps.py --build          # here (no GPU): compile tools/_diag/libqvit_hip_stamps.so
+    python tools/gemm_stamps.py [--shapes fc1_i32,fc2]   # on the GPU box
+
+Phases: prologue (first 3 stages issued, stage 0 read), DMA issue, stage wait (vmcnt + barrier),
+fragment reads + MFMA issue, epilogue, and the step-top LDS drain. Stamps cost cycles themselves;
+compare phases within one run, not against the product library's wall time.
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+DIAG = os.path.join(ROOT, "tools", "_diag")
+LIB = os.path.join(DIAG, "libqvit_hip_stamps.so")
+PHASES = ["prologue", "dma_issue", "stage_wait", "reads+mfma", "epilogue", "step_drain"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--shapes", default="fc1_i32,fc1,qkv,fc2")
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--abl", type=int, nargs="*", default=[1, 4, 5],
+                    help="with --build: also build timing-only ablation libraries (1 no DMA, "
+                         "4 contiguous L2-hot pieces, 5 per-row pieces on L2-hot rows)")
+    ap.add_argument("--bench-abl", type=int, default=0, help="time ablation library N (no stamps)")
+    a = ap.parse_args()
+    from quantized_vit_amd import build
+    if a.build:
+        print(build.build(defines=("QVIT_GEMM_STAMPS",), lib=LIB, build_dir=os.path.join(DIAG, "obj")))
+        for n in a.abl:
+            print(build.build(defines=(f"QVIT_GEMM_ABL={n}",), lib=os.path.join(DIAG, f"libqvit_hip_abl{n}.so"),
+                              build_dir=os.path.join(DIAG, f"obj_abl{n}")))
+        return
+    if a.bench_abl:
+        import torch
+        from quantized_vit_amd import _lib
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import gemm_bench
+        _lib.load(os.path.join(DIAG, f"libqvit_hip_abl{a.bench_abl}.so"))
+        for name in a.shapes.split(","):
+            M, N, K, epi = gemm_bench.SHAPES[name]
+            r = gemm_bench.run(name, M, N, K, epi, 20, torch.device("cuda:0"))
+            print(f"abl{a.bench_abl} {name:8s} {r['ms']*1e3:8.1f} us  {100*r['frac']:5.1f}% of int8 peak", flush=True)
+        return
+    import torch
+    from quantized_vit_amd import _lib
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import gemm_bench
+    lib = _lib.load(LIB)
+    lib.qvit_gemm_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.qvit_gemm_stamps.restype = ctypes.c_int
+    dev = torch.device("cuda:0")
+    buf = (ctypes.c_ulonglong * 8)()
+    for name in a.shapes.split(","):
+        M, N, K, epi = gemm_bench.SHAPES[name]
+        torch.cuda.synchronize()
+        assert lib.qvit_gemm_stamps(buf, 1) == 0
+        r = gemm_bench.run(name, M, N, K, epi, a.iters, dev)
+        torch.cuda.synchronize()
+        assert lib.qvit_gemm_stamps(buf, 0) == 0
+        waves = max(buf[7], 1)
+        per = [buf[i] / waves for i in range(6)]
+        tot = sum(per)
+        nk = K // 64
+        mfma_cyc = 32 * nk * 16  # 32 MFMAs of 16 cycles per stage, one wave alone on its SIMD
+        print(f"{name:8s} {r['ms']*1e3:7.1f} us  cycles/wave {tot:9.0f}  (MFMA floor {mfma_cyc})  " +
+              "  ".join(f"{p} {v:7.0f} ({100*v/tot:4.1f}%)" for p, v in zip(PHASES, per)), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,16 +1,82 @@
-"""Summarise a rocprofv3 --stats kernel_stats.csv: top kernels by total time (short names)."""
+"""rocprofv3 summaries.
+
+    python tools/kstats.py STATS_CSV [N]                 top kernels of a --stats kernel_stats.csv
+    python tools/kstats.py --pmc FETCH_DIR WRITE_DIR [--round r01]
+                                                        fc1 HBM traffic per launch from two PMC passes
+
+PMC conventions (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE are kilobytes per
+dispatch; on gfx950 FETCH_SIZE reports half the bytes of a 16-B-per-lane streaming read (128-B requests
+tallied at 64 B), so it is doubled; WRITE_SIZE is taken as is. Both count Infinity-Cache hits as
+fabric traffic (an upper bound on HBM bytes).
+"""
 import csv
+import glob
+import json
+import os
 import re
+import statistics
 import sys
 
-rows = list(csv.DictReader(open(sys.argv[1])))
-rows.sort(key=lambda r: -float(r["TotalDurationNs"]))
-n = int(sys.argv[2]) if len(sys.argv) > 2 else 25
-for r in rows[:n]:
-    name = r["Name"]
-    m = re.match(r"(?:void )?(?:\(anonymous namespace\)::)?([\w:<>, ]+?)\(", name)
-    short = (m.group(1) if m else name)[:70]
-    if short.startswith("Cijk"):
-        short = name[:40]
-    print(f'{float(r["TotalDurationNs"])/1e6:9.3f} ms  calls={int(r["Calls"]):5d}  avg={float(r["AverageNs"])/1e3:9.2f} us  '
-          f'{float(r["Percentage"]):5.1f}%  {short}')
+FC1_KERNEL = re.compile(r"gemm_kernel<4, 2, 1, false>")  # W4 weights, I8_GELU epilogue, K > 128
+
+
+def top(path, n=25):
+    rows = list(csv.DictReader(open(path)))
+    rows.sort(key=lambda r: -float(r["TotalDurationNs"]))
+    for r in rows[:n]:
+        name = r["Name"]
+        m = re.match(r"(?:void )?(?:\(anonymous namespace\)::)?([\w:<>, ]+?)\(", name)
+        short = (m.group(1) if m else name)[:70]
+        if short.startswith("Cijk"):
+            short = name[:40]
+        print(f'{float(r["TotalDurationNs"])/1e6:9.3f} ms  calls={int(r["Calls"]):5d}  '
+              f'avg={float(r["AverageNs"])/1e3:9.2f} us  {float(r["Percentage"]):5.1f}%  {short}')
+
+
+def pmc_values(d, counter):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {d}")
+    vals = []
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            if r.get("Counter_Name") == counter and FC1_KERNEL.search(r.get("Kernel_Name", "")):
+                vals.append(float(r["Counter_Value"]))
+    return vals
+
+
+def pmc(fetch_dir, write_dir, rnd):
+    fetch = pmc_values(fetch_dir, "FETCH_SIZE")
+    write = pmc_values(write_dir, "WRITE_SIZE")
+    if not fetch or not write:
+        raise SystemExit(f"fc1 kernel not found in PMC output (fetch {len(fetch)}, write {len(write)})")
+    f_b = 2.0 * statistics.median(fetch) * 1024
+    w_b = statistics.median(write) * 1024
+    out = {
+        "kernel": FC1_KERNEL.pattern,
+        "launches": {"fetch_pass": len(fetch), "write_pass": len(write)},
+        "fetch_size_kb_median_raw": statistics.median(fetch),
+        "write_size_kb_median_raw": statistics.median(write),
+        "fetch_bytes_per_launch": f_b,
+        "write_bytes_per_launch": w_b,
+        "traffic_bytes_per_launch": f_b + w_b,
+        "corrections": "FETCH_SIZE x2 (gfx950 64-B tally of 128-B requests), KB->B x1024; WRITE_SIZE as is",
+        "round": rnd,
+        # the profiled command: bench.py defaults (tools/profile_fc1.sh)
+        "batch": int(os.environ.get("BENCH_BATCH", "256")),
+        "model": os.environ.get("BENCH_MODEL", "vit_base_patch16_224"),
+    }
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    os.makedirs(os.path.join(root, "profiles"), exist_ok=True)
+    for name in (f"fc1_traffic_{rnd}.json", "fc1_traffic.json"):
+        with open(os.path.join(root, "profiles", name), "w") as fh:
+            json.dump(out, fh, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "--pmc":
+        rnd = sys.argv[sys.argv.index("--round") + 1] if "--round" in sys.argv else "r01"
+        pmc(sys.argv[2], sys.argv[3], rnd)
+    else:
+        top(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 25)
