@@ -21,6 +21,9 @@
  *                             int8 x int4/int8 -> int32 MFMA contraction with a fused epilogue:
  *                             d_act * d_wt * acc + bias, optionally + residual (vit_model.py:206-207),
  *                             or GELU (vit_model.py:173) + the next layer's activation quantizer.
+ *   qvit_attention            vit_model.py:133-149 (Attention.forward between qkv and proj):
+ *                             softmax(q k^T * scale) v per (image, head), fp32 out or fused with the
+ *                             proj layer's quantize_act (quant_layers.py:497) -> int8 codes.
  *
  * Conventions
  *   - Plain pointers and sizes only. All pointers are device pointers (hipMalloc'd / torch CUDA
