@@ -167,8 +167,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "int8",
-        "data": "synthetic uniform[-1,1) 224x224 images; random-init ViT-B/16 (reference init), W4 (nonlinear "
-                "quantizer, t=1) / A8 calibrated",
+        "data": f"synthetic uniform[-1,1) {img_size}x{img_size} images; random-init {args.model} (reference init), "
+                "W4 (nonlinear quantizer, t=1) / A8 calibrated",
         "config": {"workload": f"{args.model} int4w/int8a forward, batch {B} per GPU"
                                + (", RCCL all-gather of logits" if world > 1 else ""),
                    "model": args.model, "global_batch": world * B, "seq_len": model.patch_embed.num_patches + 1,

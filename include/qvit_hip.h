@@ -21,6 +21,8 @@
  *                             int8 x int4/int8 -> int32 MFMA contraction with a fused epilogue:
  *                             d_act * d_wt * acc + bias, optionally + residual (vit_model.py:206-207),
  *                             or GELU (vit_model.py:173) + the next layer's activation quantizer.
+ *   qvit_ultra_*              4-bit quantization/quant_ultra.py:8-91 + mymodel.py:62-144 (UltraNet: weight
+ *                             codes, BN folding, fused conv+BN+quantizer+maxpool blocks, YOLO decode).
  *   qvit_attention            vit_model.py:133-149 (Attention.forward between qkv and proj):
  *                             softmax(q k^T * scale) v per (image, head), fp32 out or fused with the
  *                             proj layer's quantize_act (quant_layers.py:497) -> int8 codes.
@@ -68,6 +70,11 @@ extern "C" {
 #define QVIT_EPI_I8_GELU    2  /* C[m,n]  = q_next(gelu(d_act d_wt acc + bias[n]))  (int8 codes)    */
 #define QVIT_EPI_I8         3  /* C[m,n]  = q_next(d_act d_wt acc + bias[n])        (int8 codes)    */
 #define QVIT_EPI_I32        4  /* C[m,n]  = acc                                      (int32, exact)  */
+
+/* ---- qvit_ultra_conv epilogues (UltraNet, 4-bit quantization/mymodel.py) -------------------- */
+#define QVIT_ULTRA_CODES       0  /* codes = rne(clamp(bn(acc/den), 0, 1) (2^a_bit-1))       (uint codes) */
+#define QVIT_ULTRA_CODES_POOL  1  /* the same followed by MaxPool2d(2, 2)                    (uint codes) */
+#define QVIT_ULTRA_F32         2  /* out = acc/den + bias (shift = bias)                      (fp32)       */
 
 /* ---- qvit_attention output modes -------------------------------------------------------------- */
 #define QVIT_ATT_F32        0  /* out = softmax(q k^T * scale) v                     (fp32)          */
@@ -179,6 +186,43 @@ int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda,
  *              (out_qtype, out_d, out_qm, out_t, out_levels as in qvit_gemm), ldo % 4 == 0.
  * fp32 matmuls are formed from fp16 hi/lo products with fp32 accumulation (~2^-22 relative error).
  */
+/*
+ * UltraNet (reference `4-bit quantization/`: quant_ultra.py:8-91, mymodel.py:23-144).
+ * Weight codes k_w = rne(tanh(w)/max|tanh(w)| * (2^(w_bit-1)-1)) (weight_quantize_fn, quant_ultra.py:30-56),
+ * activation codes k_a = rne(clamp(x,0,1) * (2^a_bit-1)) (activation_quantize_fn :59-73), so a
+ * Conv2d_Q on codes is the int32 contraction acc with value acc / den, den = (2^(w_bit-1)-1)(2^a_bit-1).
+ *
+ * qvit_ultra_weight_codes: w fp32 [cout][cin][ks][ks] -> codes int8 [cout_pad][kpad] in K order
+ *   (ky, kx, c), zero padded; values (nullable) = the reference's fake-quant weight k_w/(2^(w_bit-1)-1)
+ *   in w's own layout; workspace = device unsigned[1] (max |tanh| scratch).
+ * qvit_ultra_bn_fold: BatchNorm2d eval constants alpha = gamma/sqrt(var+eps), shift = beta - mean*alpha.
+ * qvit_ultra_conv0: layer 0 (mymodel.py:73-77): float image NCHW [B][3][H][W] -> conv 3x3 pad 1 with the
+ *   fake-quant weights (wvals [16][3][3][3], the `values` output of qvit_ultra_weight_codes)
+ *   -> BN (alpha, shift) -> activation quantizer -> MaxPool2d(2,2);
+ *   out = codes NHWC [B][H/2][W/2][16], 16-byte aligned.
+ * qvit_ultra_conv: layers 1..8: in = codes NHWC [B][H][W][cin] (16-B aligned), ks in {1, 3} (pad ks/2),
+ *   wcodes [round_up(cout,16)][kpad] from qvit_ultra_weight_codes; mode QVIT_ULTRA_* ; out NHWC with
+ *   row (pixel) pitch ldo: codes (ldo % 4 == 0) or fp32 (the 1x1 head, shift = its bias).
+ *   Supported (cin, ks, cout): (16,3,17..32), (32,3,49..64), (64,3,49..64), (64,1,33..48).
+ * qvit_yolo_decode: YOLOLayer eval decode (mymodel.py:47-60) of the head output NHWC [B][ny][nx][ldh]
+ *   (channel a*no + o) with anchors (device float [na][2]) and stride -> io and p, both
+ *   [B][na][ny][nx][no] (io.view(bs, -1, no) is the reference's first output).
+ */
+int qvit_ultra_weight_codes(const float* w, int64_t cout, int64_t cin, int64_t ks, int w_bit,
+                            int8_t* codes, int64_t kpad, int64_t cout_pad, float* values,
+                            unsigned* workspace, hipStream_t stream);
+int qvit_ultra_bn_fold(const float* gamma, const float* beta, const float* mean, const float* var,
+                       float eps, int64_t n, float* alpha, float* shift, hipStream_t stream);
+int qvit_ultra_conv0(const float* img, int64_t B, int64_t H, int64_t W, const float* wvals,
+                     const float* alpha, const float* shift, int a_bit, int8_t* out, hipStream_t stream);
+int qvit_ultra_conv(const int8_t* in, int64_t B, int64_t H, int64_t W, int64_t cin, int64_t ks,
+                    const int8_t* wcodes, int64_t kpad, int64_t cout, int w_bit, int a_bit,
+                    const float* alpha, const float* shift, int mode, void* out, int64_t ldo,
+                    hipStream_t stream);
+int qvit_yolo_decode(const float* head, int64_t B, int64_t ny, int64_t nx, int64_t na, int64_t no,
+                     int64_t ldh, const float* anchors, float stride, float* io, float* p,
+                     hipStream_t stream);
+
 int qvit_attention(const float* qkv, int64_t B, int64_t N, int64_t H, int64_t head_dim, int64_t ldq,
                    float scale, float in_scale, int out_mode, void* out, int64_t ldo,
                    int out_qtype, const float* out_d, const float* out_qm, const float* out_t,

@@ -34,6 +34,10 @@ EPI_I32 = 4
 ATT_F32 = 0
 ATT_I8 = 1
 
+ULTRA_CODES = 0
+ULTRA_CODES_POOL = 1
+ULTRA_F32 = 2
+
 TILE_N = 256
 TILE_K = 128
 
@@ -54,6 +58,12 @@ _SIGNATURES = {
                                 _c_p, _i64, _i64, _c_p],
     "qvit_gemm": [_c_p, _i64, _i64, _i64, _c_p, _i32, _i64, _i64, _c_p, _c_p, _c_p, _i32, _c_p, _i64,
                   _i32, _c_p, _c_p, _c_p, _i32, _c_p],
+    "qvit_ultra_weight_codes": [_c_p, _i64, _i64, _i64, _i32, _c_p, _i64, _i64, _c_p, _c_p, _c_p],
+    "qvit_ultra_bn_fold": [_c_p, _c_p, _c_p, _c_p, _f32, _i64, _c_p, _c_p, _c_p],
+    "qvit_ultra_conv0": [_c_p, _i64, _i64, _i64, _c_p, _c_p, _c_p, _i32, _c_p, _c_p],
+    "qvit_ultra_conv": [_c_p, _i64, _i64, _i64, _i64, _i64, _c_p, _i64, _i64, _i32, _i32, _c_p, _c_p, _i32, _c_p,
+                        _i64, _c_p],
+    "qvit_yolo_decode": [_c_p, _i64, _i64, _i64, _i64, _i64, _i64, _c_p, _f32, _c_p, _c_p, _c_p],
     "qvit_attention": [_c_p, _i64, _i64, _i64, _i64, _i64, _f32, _f32, _i32, _c_p, _i64, _i32, _c_p, _c_p, _c_p,
                        _i32, _c_p],
 }
@@ -199,3 +209,72 @@ def attention(qkv: torch.Tensor, B: int, N: int, H: int, head_dim: int, scale: f
                                  out.stride(0), out_qtype, _ptr(out_d), _ptr(out_qm), _ptr(out_t), out_levels,
                                  _stream(qkv.device)), "qvit_attention")
     return out
+
+
+# ---- UltraNet ---------------------------------------------------------------------------------------
+def ultra_weight_codes(w: torch.Tensor, w_bit: int, kpad: int, cout_pad: int, values: bool = False):
+    """Conv weight [cout][cin][ks][ks] -> int8 codes [cout_pad][kpad] in K order (ky, kx, c)
+    (and, with values=True, also the fake-quant weight k/(2^(w_bit-1)-1) in w's layout)."""
+    _require_gpu(w, "weight")
+    w = w.detach().float().contiguous()
+    cout, cin, ks, ks2 = w.shape
+    assert ks == ks2
+    codes = torch.empty((cout_pad, kpad), dtype=torch.int8, device=w.device)
+    vals = torch.empty_like(w) if values else None
+    ws = torch.empty(1, dtype=torch.int32, device=w.device)
+    _check(load().qvit_ultra_weight_codes(_ptr(w), cout, cin, ks, w_bit, _ptr(codes), kpad, cout_pad, _ptr(vals),
+                                          _ptr(ws), _stream(w.device)), "qvit_ultra_weight_codes")
+    return (codes, vals) if values else codes
+
+
+def ultra_bn_fold(bn, device) -> tuple:
+    n = bn.num_features
+    alpha = torch.empty(n, device=device)
+    shift = torch.empty(n, device=device)
+    g = bn.weight.detach().float().contiguous() if bn.weight is not None else None
+    b = bn.bias.detach().float().contiguous() if bn.bias is not None else None
+    _check(load().qvit_ultra_bn_fold(_ptr(g), _ptr(b), _ptr(bn.running_mean), _ptr(bn.running_var), float(bn.eps), n,
+                                     _ptr(alpha), _ptr(shift), _stream(device)), "qvit_ultra_bn_fold")
+    return alpha, shift
+
+
+def ultra_conv0(img: torch.Tensor, wvals: torch.Tensor, alpha, shift, a_bit: int) -> torch.Tensor:
+    """Layer 0: float image NCHW -> conv3x3 with fake-quant weights wvals [16][3][3][3] -> BN -> quantizer
+    -> 2x2 max pool -> NHWC codes [B][H/2][W/2][16]."""
+    _require_gpu(img, "image")
+    assert img.dtype == torch.float32 and img.is_contiguous() and img.shape[1] == 3
+    assert wvals.shape == (16, 3, 3, 3) and wvals.is_contiguous()
+    B, _, H, W = img.shape
+    out = torch.empty((B, H // 2, W // 2, 16), dtype=torch.int8, device=img.device)
+    _check(load().qvit_ultra_conv0(_ptr(img), B, H, W, _ptr(wvals), _ptr(alpha), _ptr(shift), a_bit, _ptr(out),
+                                   _stream(img.device)), "qvit_ultra_conv0")
+    return out
+
+
+def ultra_conv(x: torch.Tensor, ks: int, wcodes: torch.Tensor, cout: int, w_bit: int, a_bit: int, alpha, shift,
+               mode: int) -> torch.Tensor:
+    """NHWC codes [B][H][W][cin] -> NHWC codes (mode ULTRA_CODES / ULTRA_CODES_POOL) or fp32 (ULTRA_F32)."""
+    _require_gpu(x, "codes")
+    assert x.dtype == torch.int8 and x.is_contiguous()
+    B, H, W, cin = x.shape
+    if mode == ULTRA_CODES_POOL:
+        out = torch.empty((B, H // 2, W // 2, cout), dtype=torch.int8, device=x.device)
+    elif mode == ULTRA_CODES:
+        out = torch.empty((B, H, W, cout), dtype=torch.int8, device=x.device)
+    else:
+        out = torch.empty((B, H, W, cout), dtype=torch.float32, device=x.device)
+    _check(load().qvit_ultra_conv(_ptr(x), B, H, W, cin, ks, _ptr(wcodes), wcodes.shape[1], cout, w_bit, a_bit,
+                                  _ptr(alpha), _ptr(shift), mode, _ptr(out), cout, _stream(x.device)),
+           "qvit_ultra_conv")
+    return out
+
+
+def yolo_decode(head: torch.Tensor, na: int, no: int, anchors: torch.Tensor, stride: float):
+    """head NHWC fp32 [B][ny][nx][na*no] -> (io [B, na*ny*nx, no], p [B, na, ny, nx, no])."""
+    _require_gpu(head, "head")
+    B, ny, nx, C = head.shape
+    io = torch.empty((B, na, ny, nx, no), device=head.device)
+    p = torch.empty_like(io)
+    _check(load().qvit_yolo_decode(_ptr(head), B, ny, nx, na, no, C, _ptr(anchors), stride, _ptr(io), _ptr(p),
+                                   _stream(head.device)), "qvit_yolo_decode")
+    return io.view(B, -1, no), p

@@ -1,0 +1,168 @@
+"""Mirror of the reference's `4-bit quantization/quant_ultra.py` (DoReFa-style 4-bit quantizers of
+UltraNet): same factory / class names and forward semantics, computed on the ROCm device.
+
+  uniform_quantize(k)        quant_ultra.py:8-27   round(x * (2^k - 1)) / (2^k - 1)  (k = 1: sign, 32: identity)
+  weight_quantize_fn(w_bit)  :30-56   tanh -> / max|tanh| -> (w_bit-1)-bit uniform quantizer (HIP codes)
+  activation_quantize_fn     :59-73   clamp(x, 0, 1) -> a_bit uniform quantizer (HIP)
+  conv2d_Q_fn(w_bit)         :76-91   Conv2d_Q: conv with quantized weights
+  batchNorm2d_Q_fn / batchNorm1d_Q_fn / linear_Q_fn  :94-222 (not used by UltraNetQua; kept for API parity)
+
+The network-level fused path (conv + BN + quantizer + max pool on codes) is in ultranet.py; these
+modules are the per-layer surface. Forward-only (inference): the reference's straight-through
+backward is not provided.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+
+
+def _check_gpu(x: torch.Tensor, what: str) -> None:
+    if not x.is_cuda:
+        raise _lib.QvitError(f"{what} on {x.device}: the UltraNet path runs on a ROCm device (no CPU fallback)")
+
+
+def uniform_quantize(k):
+    """quant_ultra.py:8-27. Returns the quantizer function (the reference returns an autograd apply)."""
+
+    def qfn(x: torch.Tensor) -> torch.Tensor:
+        if k == 32:
+            return x
+        if k == 1:
+            return torch.sign(x)
+        n = float(2 ** k - 1)
+        return torch.round(x * n) / n
+
+    return qfn
+
+
+def _round_up(v: int, m: int) -> int:
+    return (v + m - 1) // m * m
+
+
+def weight_codes(weight: torch.Tensor, w_bit: int, kpad: int = None, cout_pad: int = None) -> torch.Tensor:
+    """Integer weight codes of weight_quantize_fn (HIP), [cout_pad][kpad] in K order (ky, kx, c)."""
+    _check_gpu(weight, "weight")
+    w4 = weight if weight.dim() == 4 else weight.reshape(weight.shape[0], -1, 1, 1)
+    cout, cin, ks, _ = w4.shape
+    kpad = kpad or _round_up(ks * ks * cin, 16)
+    cout_pad = cout_pad or cout
+    return _lib.ultra_weight_codes(w4, w_bit, kpad, cout_pad)
+
+
+class weight_quantize_fn(nn.Module):
+    """quant_ultra.py:30-56."""
+
+    def __init__(self, w_bit):
+        super().__init__()
+        assert w_bit <= 8 or w_bit == 32
+        self.w_bit = w_bit
+        self.uniform_q = uniform_quantize(k=w_bit - 1)
+
+    def forward(self, x):
+        if self.w_bit == 32:
+            return x
+        if self.w_bit == 1:   # reference behaviour kept as is (its k = 0 quantizer divides by zero)
+            E = torch.mean(torch.abs(x)).detach()
+            return (self.uniform_q(x / E) + 1) / 2 * E
+        _check_gpu(x, "weight")
+        w4 = x if x.dim() == 4 else x.reshape(x.shape[0], -1, 1, 1)
+        cout, cin, ks, _ = w4.shape
+        _, vals = _lib.ultra_weight_codes(w4, self.w_bit, _round_up(ks * ks * cin, 16), cout, values=True)
+        return vals.reshape(x.shape)   # round(.)/n (:20), divided on the device as IEEE fp32
+
+
+class activation_quantize_fn(nn.Module):
+    """quant_ultra.py:59-73."""
+
+    def __init__(self, a_bit):
+        super().__init__()
+        assert a_bit <= 8 or a_bit == 32
+        self.a_bit = a_bit
+        self.uniform_q = uniform_quantize(k=a_bit)
+
+    def forward(self, x):
+        if self.a_bit == 32:
+            return x
+        _check_gpu(x, "activation")
+        if self.a_bit > 7:   # levels beyond the int8 code range: the reference arithmetic on the device
+            return self.uniform_q(torch.clamp(x, 0, 1))
+        return _lib.fake_quant_f32(x, _lib.QT_ULTRA_ACT, None, None, None, 2 ** self.a_bit - 1).reshape(x.shape)
+
+
+def conv2d_Q_fn(w_bit):
+    """quant_ultra.py:76-91."""
+
+    class Conv2d_Q(nn.Conv2d):
+        def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, dilation=1, groups=1,
+                     bias=True):
+            super().__init__(in_channels, out_channels, kernel_size, stride, padding, dilation, groups, bias)
+            self.w_bit = w_bit
+            self.quantize_fn = weight_quantize_fn(w_bit=w_bit)
+
+        def forward(self, input, order=None):
+            weight_q = self.quantize_fn(self.weight)
+            return F.conv2d(input, weight_q, self.bias, self.stride, self.padding, self.dilation, self.groups)
+
+    return Conv2d_Q
+
+
+def batchNorm2d_Q_fn(w_bit):
+    """quant_ultra.py:94-132 (BN with quantized folded scale/shift)."""
+
+    class BatchNorm2d_Q(nn.BatchNorm2d):
+        def __init__(self, num_features, eps=1e-5, momentum=0.1, affine=True, track_running_stats=True):
+            super().__init__(num_features, eps, momentum, affine, track_running_stats)
+            self.w_bit = w_bit
+            self.quantize_fn = uniform_quantize(k=w_bit)
+
+        def forward(self, input):
+            gamma, var, mean, eps, bias = self.weight, self.running_var, self.running_mean, self.eps, self.bias
+            w = gamma / (torch.sqrt(var) + eps)
+            b = bias - (mean / (torch.sqrt(var) + eps)) * gamma
+            w = torch.clamp(w, -1, 1) / 2 + 0.5
+            w_q = 2 * self.quantize_fn(w) - 1
+            b = torch.clamp(b, -1, 1) / 2 + 0.5
+            b_q = 2 * self.quantize_fn(b) - 1
+            return F.batch_norm(input, running_mean=mean * 0, running_var=torch.sign(torch.abs(var) + 1),
+                                weight=w_q, bias=b_q, eps=eps * 0)
+
+    return BatchNorm2d_Q
+
+
+def batchNorm1d_Q_fn(w_bit):
+    """quant_ultra.py:135-207 (eval form)."""
+
+    class BatchNorm1d_Q(nn.BatchNorm1d):
+        def __init__(self, num_features, eps=1e-5, momentum=0.1, affine=True, track_running_stats=True):
+            super().__init__(num_features, eps, momentum, affine, track_running_stats)
+            self.w_bit = w_bit
+            self.quantize_fn = uniform_quantize(k=w_bit)
+
+        def forward(self, input):
+            self._check_input_dim(input)
+            gamma, var, mean, eps, bias = self.weight, self.running_var, self.running_mean, self.eps, self.bias
+            w = gamma / (torch.sqrt(var) + eps)
+            b = bias - (mean / (torch.sqrt(var) + eps)) * gamma
+            return F.batch_norm(input, mean * 0, torch.sign(var + 1), w, b,
+                                self.training or not self.track_running_stats, self.momentum or 0.0, eps * 0)
+
+    return BatchNorm1d_Q
+
+
+def linear_Q_fn(w_bit):
+    """quant_ultra.py:210-222."""
+
+    class Linear_Q(nn.Linear):
+        def __init__(self, in_features, out_features, bias=True):
+            super().__init__(in_features, out_features, bias)
+            self.w_bit = w_bit
+            self.quantize_fn = weight_quantize_fn(w_bit=w_bit)
+
+        def forward(self, input):
+            return F.linear(input, self.quantize_fn(self.weight), self.bias)
+
+    return Linear_Q

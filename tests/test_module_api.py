@@ -99,3 +99,29 @@ def test_saturation_level_host_formula():
 
 def test_initialize_quant_layer_ignores_other_modules():
     initialize_quant_layer(nn.Linear(2, 2), num_bits=4)   # no-op, as in the reference (:419-420)
+
+
+def test_ultranet_state_dict_keys_match_reference():
+    """UltraNetQua (mymodel.py:62-130): nn.Sequential of Conv2d_Q / BatchNorm2d / activation_quantize_fn /
+    MaxPool2d, so a reference checkpoint's keys are layers.{i}.*."""
+    from quantized_vit_amd.ultranet import UltraNetQua
+    m = UltraNetQua()
+    keys = set(m.state_dict().keys())
+    conv_idx = [0, 4, 8, 12, 16, 19, 22, 25]
+    want = set()
+    for i in conv_idx:
+        want.add(f"layers.{i}.weight")
+        for k in ("weight", "bias", "running_mean", "running_var", "num_batches_tracked"):
+            want.add(f"layers.{i + 1}.{k}")
+    want |= {"layers.28.weight", "layers.28.bias"}
+    assert keys == want
+    assert m.layers[28].weight.shape == (36, 64, 1, 1) and m.layers[0].weight.shape == (16, 3, 3, 3)
+    assert m.yololayer.na == 6 and m.yololayer.no == 6
+
+
+def test_ultranet_cpu_forward_fails_loudly():
+    from quantized_vit_amd import _lib
+    from quantized_vit_amd.ultranet import UltraNetQua
+    m = UltraNetQua().eval()
+    with pytest.raises(_lib.QvitError):
+        m(torch.rand(1, 3, 64, 64))
