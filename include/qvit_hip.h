@@ -164,14 +164,30 @@ int qvit_layernorm_quant_i8(const float* x, int64_t rows, int64_t cols, int64_t 
  *   N      : true out features (<= npad); outputs for n >= N are not written.
  *   d_act, d_wt : device float[1] scales; bias : device float[npad] (padded) or NULL.
  *   C      : fp32 / int8 / int32 [M][ldc] per epilogue; ldc % 4 == 0 (fp32/int32), % 16 (int8).
- *   For QVIT_EPI_I8*: the next layer's quantizer (out_qtype, out_d, out_qm, out_t, out_levels).
+ *   For QVIT_EPI_I8*: the next layer's quantizer (out_qtype, out_d, out_qm, out_t, out_levels) and an
+ *   optional code table (qvit_epi_table_build, NULL -> per-element evaluation).
  */
 int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda,
               const void* Wp, int wfmt, int64_t N, int64_t npad,
               const float* d_act, const float* d_wt, const float* bias,
               int epilogue, void* C, int64_t ldc,
               int out_qtype, const float* out_d, const float* out_qm, const float* out_t,
-              int out_levels, hipStream_t stream);
+              int out_levels, const void* epi_table, hipStream_t stream);
+
+/*
+ * Code table for the int8 epilogues (optional `epi_table` of qvit_gemm; 16-byte aligned,
+ * QVIT_EPI_TABLE_BYTES(nb) bytes). The output code of QVIT_EPI_I8 / QVIT_EPI_I8_GELU is a piecewise
+ * constant function of the pre-activation v = d_act d_wt acc + bias; the table holds it exactly over
+ * nb uniform buckets of width w starting at v_lo (w must be below the smallest distance between two
+ * of its change points, and the function constant beyond both ends). The device builds it by bisection
+ * with the epilogue's own arithmetic and validates it; qvit_gemm uses it only if valid (else the
+ * direct per-element evaluation runs), so results never depend on the choice of (v_lo, w, nb).
+ */
+#define QVIT_EPI_TABLE_MAX_NB 3800
+#define QVIT_EPI_TABLE_BYTES(nb) (16 + 8 * (nb))
+int qvit_epi_table_build(int epilogue, int out_qtype, const float* out_d, const float* out_qm,
+                         const float* out_t, int out_levels, float v_lo, float w, int64_t nb,
+                         void* table, hipStream_t stream);
 
 /*
  * Attention core between the qkv and proj QuantizeLinear layers of Attention.forward

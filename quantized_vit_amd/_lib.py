@@ -38,6 +38,8 @@ ULTRA_CODES = 0
 ULTRA_CODES_POOL = 1
 ULTRA_F32 = 2
 
+EPI_TABLE_MAX_NB = 3800
+
 TILE_N = 256
 TILE_K = 128
 
@@ -57,7 +59,8 @@ _SIGNATURES = {
     "qvit_layernorm_quant_i8": [_c_p, _i64, _i64, _i64, _c_p, _c_p, _f32, _i32, _c_p, _c_p, _c_p, _i32,
                                 _c_p, _i64, _i64, _c_p],
     "qvit_gemm": [_c_p, _i64, _i64, _i64, _c_p, _i32, _i64, _i64, _c_p, _c_p, _c_p, _i32, _c_p, _i64,
-                  _i32, _c_p, _c_p, _c_p, _i32, _c_p],
+                  _i32, _c_p, _c_p, _c_p, _i32, _c_p, _c_p],
+    "qvit_epi_table_build": [_i32, _i32, _c_p, _c_p, _c_p, _i32, _f32, _f32, _i64, _c_p, _c_p],
     "qvit_ultra_weight_codes": [_c_p, _i64, _i64, _i64, _i32, _c_p, _i64, _i64, _c_p, _c_p, _c_p],
     "qvit_ultra_bn_fold": [_c_p, _c_p, _c_p, _c_p, _f32, _i64, _c_p, _c_p, _c_p],
     "qvit_ultra_conv0": [_c_p, _i64, _i64, _i64, _c_p, _c_p, _c_p, _i32, _c_p, _c_p],
@@ -191,12 +194,21 @@ def layernorm_quant_i8(x2d: torch.Tensor, gamma: Optional[torch.Tensor], beta: O
 def gemm(A: torch.Tensor, M: int, K: int, packed: torch.Tensor, wfmt: int, N: int, npad: int,
          d_act: Optional[torch.Tensor], d_wt: Optional[torch.Tensor], bias_pad: Optional[torch.Tensor],
          epilogue: int, C: torch.Tensor, out_qtype: int = 0, out_d=None, out_qm=None, out_t=None,
-         out_levels: int = 0) -> torch.Tensor:
+         out_levels: int = 0, epi_table: Optional[torch.Tensor] = None) -> torch.Tensor:
     _require_gpu(A, "codes")
     _check(load().qvit_gemm(_ptr(A), M, K, A.stride(0), _ptr(packed), wfmt, N, npad, _ptr(d_act), _ptr(d_wt),
                             _ptr(bias_pad), epilogue, _ptr(C), C.stride(0), out_qtype, _ptr(out_d), _ptr(out_qm),
-                            _ptr(out_t), out_levels, _stream(A.device)), "qvit_gemm")
+                            _ptr(out_t), out_levels, _ptr(epi_table), _stream(A.device)), "qvit_gemm")
     return C
+
+
+def epi_table_build(epilogue: int, out_qtype: int, out_d, out_qm, out_t, out_levels: int, v_lo: float, w: float,
+                    nb: int, device: torch.device) -> torch.Tensor:
+    """Code table of an int8 GEMM epilogue (qvit_epi_table_build); validity is decided on the device."""
+    table = torch.empty(16 + 8 * nb, dtype=torch.uint8, device=device)
+    _check(load().qvit_epi_table_build(epilogue, out_qtype, _ptr(out_d), _ptr(out_qm), _ptr(out_t), out_levels,
+                                       v_lo, w, nb, _ptr(table), _stream(device)), "qvit_epi_table_build")
+    return table
 
 
 def attention(qkv: torch.Tensor, B: int, N: int, H: int, head_dim: int, scale: float, out: torch.Tensor,

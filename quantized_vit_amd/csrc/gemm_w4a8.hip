@@ -22,6 +22,8 @@
 //   rows, 64-B int8 code rows, one inlined copy of the (GELU +) quantizer per element slot.
 // Grid: one block per output tile; blockIdx is remapped so that consecutive tiles (same activation
 //   panel, different weight panels) share an XCD and its L2.
+#include <cmath>
+#include <cstddef>
 #include <type_traits>
 
 #include "qvit_common.h"
@@ -102,7 +104,94 @@ struct EpiArgs {
   const float* out_qm;
   const float* out_t;
   int out_levels;
+  const int8_t* table;  // optional code table for the I8 epilogues (qvit_epi_table_build)
 };
+
+// ---- code table of the int8 epilogues --------------------------------------------------------------
+// The epilogue's output code as a function of its fp32 pre-activation v = alpha*acc + bias,
+//   F(v) = quant_code(gelu_ref(v))  (EPI_I8_GELU)   or   quant_code(v)  (EPI_I8),
+// is piecewise constant with at most 2L+1 values. Buckets of uniform width in v, each narrower than the
+// smallest distance between two change points of F, hold (threshold, code below, code above):
+//   F(v) = v >= thr ? hi : lo      for every v the index formula maps to that bucket,
+// and the range [v_lo, v_lo + nb w) is chosen so F is constant beyond either end (the clamped index
+// then still reads the right code). The table is built on the device by bisection with the very same F
+// the direct epilogue evaluates, and validated (both ends constant, no bucket whose end codes differ
+// by more than one); an invalid table makes the epilogue fall back to the direct computation.
+struct EpiTableHdr {
+  float v_lo;
+  float inv_w;
+  int nb;
+  int valid;
+};
+struct EpiTableEnt {
+  float thr;
+  int8_t lo, hi;
+  int16_t pad;
+};
+constexpr int EPI_TABLE_LDS_OFF = 4 * 32 * 68 * 4;  // after the 4 waves' accumulator staging areas
+
+QVIT_DEV int epi_bucket(float v, float v_lo, float inv_w, int nb) {
+  const float f = __fmul_rn(__fsub_rn(v, v_lo), inv_w);
+  return (int)fminf(fmaxf(f, 0.f), (float)(nb - 1));  // NaN -> 0
+}
+
+QVIT_DEV float epi_F(float v, int gelu, const QParams& qp) { return quant_code(gelu ? gelu_ref(v) : v, qp); }
+
+// float <-> totally ordered int key (for bisection over representable floats)
+QVIT_DEV int fkey(float f) {
+  const int i = __float_as_int(f);
+  return i >= 0 ? i : (int)(0x80000000u - (unsigned)i);
+}
+QVIT_DEV float funkey(int k) { return __int_as_float(k >= 0 ? k : (int)(0x80000000u - (unsigned)k)); }
+
+__global__ void epi_table_kernel(int gelu, int out_qtype, const float* out_d, const float* out_qm, const float* out_t,
+                                 int out_levels, float v_lo, float inv_w, int nb, int8_t* table) {
+  const QParams qp = load_qparams(out_qtype, out_d, out_qm, out_t, out_levels);
+  EpiTableHdr* hdr = reinterpret_cast<EpiTableHdr*>(table);
+  EpiTableEnt* ent = reinterpret_cast<EpiTableEnt*>(table + sizeof(EpiTableHdr));
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j == 0) {
+    hdr->v_lo = v_lo;
+    hdr->inv_w = inv_w;
+    hdr->nb = nb;
+  }
+  if (j >= nb) return;
+  // smallest float mapped to bucket >= j, and the largest float of bucket j
+  auto first_at_least = [&](int b) {
+    int lo = fkey(-3.0e38f), hi = fkey(3.0e38f);
+    while (lo < hi) {
+      const int mid = lo + ((hi - lo) >> 1);
+      if (epi_bucket(funkey(mid), v_lo, inv_w, nb) >= b) hi = mid;
+      else lo = mid + 1;
+    }
+    return lo;
+  };
+  const int ks = (j == 0) ? fkey(-3.0e38f) : first_at_least(j);
+  const int ke = (j == nb - 1) ? fkey(3.0e38f) : first_at_least(j + 1) - 1;
+  const float cs = epi_F(funkey(ks), gelu, qp), ce = epi_F(funkey(ke), gelu, qp);
+  bool ok = fabsf(cs - ce) <= 1.f && !(isnan(cs) || isnan(ce));
+  float thr = INFINITY;
+  if (cs != ce) {  // the one change point inside the bucket: first v whose code differs from cs
+    int lo = ks, hi = ke;
+    while (lo < hi) {
+      const int mid = lo + ((hi - lo) >> 1);
+      if (epi_F(funkey(mid), gelu, qp) != cs) hi = mid;
+      else lo = mid + 1;
+    }
+    thr = funkey(lo);
+  }
+  if (j == 0 || j == nb - 1) {  // F must be constant beyond the table's ends
+    const float far = epi_F(j == 0 ? -1.0e30f : 1.0e30f, gelu, qp);
+    if (far != (j == 0 ? cs : ce)) ok = false;
+  }
+  EpiTableEnt e;
+  e.thr = thr;
+  e.lo = to_i8_sat(cs);
+  e.hi = to_i8_sat(ce);
+  e.pad = 0;
+  ent[j] = e;
+  if (!ok) atomicAnd(&hdr->valid, 0);
+}
 
 // Diagnostic build only (-DQVIT_GEMM_STAMPS, tools/gemm_stamps.py): per-phase s_memtime cycle sums.
 // In the product library these macros are empty.
@@ -358,6 +447,23 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   if (EPI != QVIT_EPI_I32 && ep.bias != nullptr) b4 = *reinterpret_cast<const float4*>(ep.bias + n);
   if (EPI == QVIT_EPI_I8 || EPI == QVIT_EPI_I8_GELU)
     qp = load_qparams(ep.out_qtype, ep.out_d, ep.out_qm, ep.out_t, ep.out_levels);
+  // code table (if given and valid) -> LDS behind the staging areas; the flag is wave-uniform
+  bool use_table = false;
+  float t_vlo = 0.f, t_invw = 0.f;
+  int t_nb = 1;
+  const EpiTableEnt* tl = reinterpret_cast<const EpiTableEnt*>(smem + EPI_TABLE_LDS_OFF);
+  if ((EPI == QVIT_EPI_I8 || EPI == QVIT_EPI_I8_GELU) && ep.table != nullptr) {
+    const EpiTableHdr h = *reinterpret_cast<const EpiTableHdr*>(ep.table);
+    use_table = h.valid != 0;
+    if (use_table) {
+      t_vlo = h.v_lo;
+      t_invw = h.inv_w;
+      t_nb = h.nb;
+      const v4i* src = reinterpret_cast<const v4i*>(ep.table + sizeof(EpiTableHdr));
+      v4i* dst = reinterpret_cast<v4i*>(smem + EPI_TABLE_LDS_OFF);
+      for (int i = tid; i < (t_nb + 1) / 2; i += G::NT) dst[i] = src[i];
+    }
+  }
 
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -400,6 +506,24 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
           const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
           float v[4], k[4];
           bool need[4];
+          if (use_table) {
+            uint32_t word = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float vj = alpha * (float)a4[j] + bb[j];
+              const EpiTableEnt e = tl[epi_bucket(vj, t_vlo, t_invw, t_nb)];
+              const int8_t c = vj >= e.thr ? e.hi : e.lo;
+              word |= ((uint32_t)(uint8_t)c) << (8 * j);
+            }
+            int8_t* dst = reinterpret_cast<int8_t*>(C) + (int64_t)m * ldc + n;
+            if (nfull) {
+              *reinterpret_cast<uint32_t*>(dst) = word;
+            } else {
+              for (int j = 0; j < 4; ++j)
+                if (n + j < N) dst[j] = (int8_t)((word >> (8 * j)) & 0xff);
+            }
+            continue;
+          }
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             v[j] = alpha * (float)a4[j] + bb[j];
@@ -460,10 +584,31 @@ int dispatch_epi(int epilogue, const int8_t* A, int64_t M, int64_t K, int64_t ld
 
 }  // namespace
 
+extern "C" int qvit_epi_table_build(int epilogue, int out_qtype, const float* out_d, const float* out_qm,
+                                    const float* out_t, int out_levels, float v_lo, float w, int64_t nb, void* table,
+                                    hipStream_t stream) {
+  if (!table) return QVIT_ENULL;
+  if (epilogue != QVIT_EPI_I8 && epilogue != QVIT_EPI_I8_GELU) return QVIT_EINVAL;
+  if (nb < 1 || nb > QVIT_EPI_TABLE_MAX_NB || !(w > 0.f) || !std::isfinite(v_lo) || !std::isfinite(v_lo + w * nb))
+    return QVIT_EINVAL;
+  const int q = out_qtype & 0xff;
+  if (q != QVIT_QT_LINEAR && q != QVIT_QT_NONLINEAR && q != QVIT_QT_ULTRA_ACT) return QVIT_EINVAL;
+  if (q == QVIT_QT_ULTRA_ACT ? (out_levels < 1 || out_levels > 127) : (!out_d || !out_qm)) return QVIT_EINVAL;
+  if (((uintptr_t)table) & 15) return QVIT_EALIGN;
+  const int one = 1;
+  hipError_t e = hipMemcpyAsync(reinterpret_cast<int8_t*>(table) + offsetof(EpiTableHdr, valid), &one, sizeof(int),
+                                hipMemcpyHostToDevice, stream);
+  if (e != hipSuccess) return qvit_hip_status(e);
+  hipLaunchKernelGGL(epi_table_kernel, dim3((unsigned)((nb + 63) / 64)), dim3(64), 0, stream,
+                     epilogue == QVIT_EPI_I8_GELU ? 1 : 0, out_qtype, out_d, out_qm, out_t, out_levels, v_lo, 1.0f / w,
+                     (int)nb, reinterpret_cast<int8_t*>(table));
+  return qvit_hip_status(hipGetLastError());
+}
+
 extern "C" int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int wfmt, int64_t N,
                          int64_t npad, const float* d_act, const float* d_wt, const float* bias, int epilogue,
                          void* C, int64_t ldc, int out_qtype, const float* out_d, const float* out_qm,
-                         const float* out_t, int out_levels, hipStream_t stream) {
+                         const float* out_t, int out_levels, const void* epi_table, hipStream_t stream) {
   if (!A || !Wp || !C) return QVIT_ENULL;
   if (wfmt != QVIT_W4 && wfmt != QVIT_W8) return QVIT_EINVAL;
   if (M < 0 || K <= 0 || K % KTILE || lda < K || N <= 0 || npad < N || npad % BN) return QVIT_EINVAL;
@@ -483,7 +628,9 @@ extern "C" int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda, con
   if (epilogue != QVIT_EPI_I32 && (!d_act || !d_wt)) return QVIT_ENULL;
   if (bias && (((uintptr_t)bias) & 15)) return QVIT_EALIGN;
   if (M == 0) return QVIT_OK;
-  EpiArgs ep{d_act, d_wt, bias, out_qtype, out_d, out_qm, out_t, out_levels};
+  if (epi_table && (((uintptr_t)epi_table) & 15)) return QVIT_EALIGN;
+  EpiArgs ep{d_act, d_wt, bias, out_qtype, out_d, out_qm, out_t, out_levels,
+             (i8out ? reinterpret_cast<const int8_t*>(epi_table) : nullptr)};
   if (wfmt == QVIT_W4) return dispatch_epi<QVIT_W4>(epilogue, A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
   return dispatch_epi<QVIT_W8>(epilogue, A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
 }

@@ -277,6 +277,8 @@ class QuantizeMixin:
             plan.bias_pad = _lib.pad_bias(bias, n, npad, dev)
             # |output| <= d_act d_wt sum_k |a_k||w_k| + |bias| <= d_act d_wt K L_a L_w + max|bias|
             plan.extra["out_bound"] = abs(s[3] * s[0]) * k * abs(la) * abs(lw) + s[-1]
+        if wa:   # host copies of the activation quantizer's scalars (epilogue code tables of the producer)
+            plan.extra["act_host"] = (qt, s[3], s[4], s[5] if t_act is not None else 1.0, la)
         else:
             wq = _lib.fake_quant_f32(self.weight.detach().float(), qt, d_wt, qm_wt, t_wt)
             plan.w_fakequant = wq
@@ -307,7 +309,8 @@ class QuantizeMixin:
             nplan = next_layer.quant_plan()
             if out is None:
                 out = torch.empty((M, _round_up(plan.n, 16)), dtype=torch.int8, device=dev)
-            oq = dict(out_qtype=nplan.qtype, out_d=nplan.d_act, out_qm=nplan.qm_act, out_t=nplan.t_act)
+            oq = dict(out_qtype=nplan.qtype, out_d=nplan.d_act, out_qm=nplan.qm_act, out_t=nplan.t_act,
+                      epi_table=epilogue_table(nplan, epilogue))
         elif epilogue == _lib.EPI_I32:
             if out is None:
                 out = torch.empty((M, _round_up(plan.n, 4)), dtype=torch.int32, device=dev)
@@ -316,6 +319,68 @@ class QuantizeMixin:
         _lib.gemm(codes, M, plan.kpad, plan.packed, plan.wfmt, plan.n, plan.npad, plan.d_act, plan.d_wt,
                   plan.bias_pad, epilogue, out, **oq)
         return out
+
+
+_GELU_MAX_SLOPE = 1.1289   # max of d/dv [v Phi(v)] (at v ~ 1.41)
+
+
+def _gelu(v: float) -> float:
+    return 0.5 * v * (1.0 + math.erf(v / math.sqrt(2.0)))
+
+
+def epilogue_table_geometry(qtype: int, d: float, qm: float, t: float, level: float, gelu: bool):
+    """(v_lo, w, nb) of the int8-epilogue code table for an activation quantizer (host scalars), or None
+    when the table would be too large (the GEMM then evaluates every element directly). Only the
+    speed depends on this choice: the device validates the table and falls back on its own."""
+    if qtype == _lib.QT_ULTRA_ACT or not (d > 0 and math.isfinite(d) and math.isfinite(qm) and qm != 0):
+        return None
+    L = int(abs(level))
+    if L < 1 or L > 127:
+        return None
+    p = (lambda x: x) if qtype == _lib.QT_LINEAR else (lambda x: x ** (1.0 / t) if x > 0 else 0.0)
+    if qtype == _lib.QT_NONLINEAR and not (t > 0 and math.isfinite(t)):
+        return None
+    # magnitude thresholds of the codes 1..L in x = gelu(v) (or v): x_k = p((k - 1/2) d), capped at |q_m|
+    xs = [min(p((k - 0.5) * d), abs(qm)) for k in range(1, L + 1)]
+    gaps = [b - a for a, b in zip(xs, xs[1:]) if b > a]
+    min_gap = min(gaps + [2.0 * xs[0]])   # change points +-x_1 around the zero code are 2 x_1 apart
+    x_sat, x_one = xs[-1], xs[0]
+    if gelu:
+        lo_v, hi_v = 0.0, max(1.0, x_sat)      # gelu(v) >= x_sat: v_hi
+        while _gelu(hi_v) < x_sat * 1.02:
+            hi_v *= 1.5
+        v_hi = hi_v + 0.05
+        if x_one >= 0.17:                       # min gelu = -0.17: no negative codes
+            v_lo = -0.05
+        else:                                   # most negative v with |gelu(v)| >= x_1
+            a, b = -40.0, -0.7518
+            for _ in range(80):
+                mid = 0.5 * (a + b)
+                if abs(_gelu(mid)) >= x_one * 0.98:
+                    b = mid
+                else:
+                    a = mid
+            v_lo = a - 0.05
+        w = 0.8 * min_gap / _GELU_MAX_SLOPE
+    else:
+        v_hi, v_lo = x_sat * 1.02 + 1e-3, -(x_sat * 1.02 + 1e-3)
+        w = 0.8 * min_gap
+    nb = int(math.ceil((v_hi - v_lo) / w)) + 1
+    if nb > _lib.EPI_TABLE_MAX_NB:
+        return None
+    return v_lo, w, nb
+
+
+def epilogue_table(nplan: QuantPlan, epilogue: int) -> Optional[torch.Tensor]:
+    """Device code table for a GEMM epilogue that quantizes with `nplan`'s activation quantizer (cached
+    on that plan: it depends only on the quantizer's scalars)."""
+    key = "epi_table_gelu" if epilogue == _lib.EPI_I8_GELU else "epi_table"
+    if key not in nplan.extra:
+        host = nplan.extra.get("act_host")
+        geo = epilogue_table_geometry(*host, gelu=epilogue == _lib.EPI_I8_GELU) if host else None
+        nplan.extra[key] = None if geo is None else _lib.epi_table_build(
+            epilogue, nplan.qtype, nplan.d_act, nplan.qm_act, nplan.t_act, 0, geo[0], geo[1], geo[2], nplan.device)
+    return nplan.extra[key]
 
 
 def initialize_quant_layer(layer, num_bits: int = 16,

@@ -56,16 +56,16 @@ def test_argument_validation_without_launch(lib):
     fake = ctypes.c_void_p(0x1000)   # never dereferenced: validation rejects before any launch
     # NULL operands
     assert lib.qvit_gemm(None, 16, 128, 128, fake, 4, 16, 256, fake, fake, None, 0, fake, 16, 0, None, None,
-                         None, 0, None) == -3
+                         None, 0, None, None) == -3
     # K not a multiple of the tile
     assert lib.qvit_gemm(fake, 16, 100, 128, fake, 4, 16, 256, fake, fake, None, 0, fake, 16, 0, None, None,
-                         None, 0, None) == -1
+                         None, 0, None, None) == -1
     # bad weight format
     assert lib.qvit_gemm(fake, 16, 128, 128, fake, 5, 16, 256, fake, fake, None, 0, fake, 16, 0, None, None,
-                         None, 0, None) == -1
+                         None, 0, None, None) == -1
     # misaligned activation stride
     assert lib.qvit_gemm(fake, 16, 128, 136, fake, 4, 16, 256, fake, fake, None, 0, fake, 16, 0, None, None,
-                         None, 0, None) == -2
+                         None, 0, None, None) == -2
     # bad quantizer enum
     assert lib.qvit_quantize_act_i8(fake, 4, 16, 16, 7, fake, fake, None, 0, fake, 16, 16, None) == -1
     # kpad not a multiple of 16

@@ -135,6 +135,62 @@ def test_gemm_int8_code_epilogue(dev, gelu, qt, t):
     assert (diff > 0).float().mean() <= 2e-4
 
 
+def _epi_gemm(dev, gelu, qt, t, table_mode, M=4096, N=768, K=256, seed=5, dn=1.4 / 127, qmn=1.4):
+    """int8-code epilogue on random codes; table_mode: None (direct), "auto" (the plan geometry) or
+    "bad" (a table whose range is far too narrow -> must be rejected on the device)."""
+    from quantized_vit_amd.quant_layers import epilogue_table_geometry, saturation_level
+    g = torch.Generator().manual_seed(seed)
+    a = torch.randint(-127, 128, (M, K), generator=g)
+    w = torch.randint(-7, 8, (N, K), generator=g)
+    bias = torch.randn(N, generator=g) * 0.5
+    packed, npad, kpad = pack_codes(w, _lib.W4, dev)
+    bias_pad = _lib.pad_bias(bias.to(dev), N, npad, dev)
+    qtc = QT[qt]
+    tt = t if qt == O.NONLINEAR else 1.0
+    if qt == O.NONLINEAR:
+        dn = qmn ** t / 127
+    epi = _lib.EPI_I8_GELU if gelu else _lib.EPI_I8
+    kw = dict(out_qtype=qtc, out_d=_p(dn, dev), out_qm=_p(qmn, dev), out_t=_p(t, dev) if qt == O.NONLINEAR else None)
+    table = None
+    if table_mode is not None:
+        L = saturation_level(qtc, dn, qmn, tt)
+        geo = epilogue_table_geometry(qtc, dn, qmn, tt, L, gelu)
+        assert geo is not None
+        if table_mode == "bad":
+            geo = (-0.01, geo[1], 4)
+        table = _lib.epi_table_build(epi, qtc, kw["out_d"], kw["out_qm"], kw["out_t"], 0, *geo, dev)
+    out = torch.empty((M, N), dtype=torch.int8, device=dev)
+    _lib.gemm(act_buffer(a, kpad, dev), M, kpad, packed, _lib.W4, N, npad, _p(0.004, dev), _p(0.0011, dev),
+              bias_pad, epi, out, epi_table=table, **kw)
+    torch.cuda.synchronize()
+    valid = None if table is None else int(table[12:16].view(torch.int32).item())
+    return out.cpu(), valid
+
+
+@pytest.mark.parametrize("gelu", [False, True])
+@pytest.mark.parametrize("qt,t", [(O.LINEAR, 1.0), (O.NONLINEAR, 1.0), (O.NONLINEAR, 0.8), (O.NONLINEAR, 1.25)])
+def test_epilogue_code_table_equals_direct(dev, gelu, qt, t):
+    """The table-driven int8 epilogue re-expresses the per-element one (3.1 M codes spanning the
+    quantizer's whole range, both signs, saturation). The fp32 GELU is monotone only up to rounding:
+    where it zig-zags by an ulp across a change point, bisection picks one of the adjacent transitions,
+    so a code may differ at such a point (measured: 0-4 in 3.1 M) — the same tie-level class as the
+    GPU-vs-CPU bar (2e-4 against the oracle); bound it at 1e-5 of codes, off by one."""
+    direct, _ = _epi_gemm(dev, gelu, qt, t, None)
+    tabled, valid = _epi_gemm(dev, gelu, qt, t, "auto")
+    assert valid == 1
+    assert len(torch.unique(direct)) > 100 or not gelu
+    d = (direct.to(torch.int32) - tabled.to(torch.int32)).abs()
+    assert d.max().item() <= 1
+    assert (d > 0).float().mean().item() <= 1e-5
+
+
+def test_epilogue_code_table_rejected_when_invalid(dev):
+    direct, _ = _epi_gemm(dev, True, O.NONLINEAR, 1.0, None)
+    tabled, valid = _epi_gemm(dev, True, O.NONLINEAR, 1.0, "bad")
+    assert valid == 0
+    assert torch.equal(direct, tabled)
+
+
 def _quant_inputs(g, n=300_000, scale=0.6):
     x = torch.randn(n, generator=g) * scale
     x[:1000] = 0.0
