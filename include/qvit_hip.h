@@ -184,7 +184,7 @@ int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda,
  * direct per-element evaluation runs), so results never depend on the choice of (v_lo, w, nb).
  */
 #define QVIT_EPI_TABLE_MAX_NB 3800
-#define QVIT_EPI_TABLE_BYTES(nb) (16 + 8 * (nb))
+#define QVIT_EPI_TABLE_BYTES(nb) ((16 + 8 * (nb) + 1023) / 1024 * 1024)  /* staged in 1-KiB pieces */
 int qvit_epi_table_build(int epilogue, int out_qtype, const float* out_d, const float* out_qm,
                          const float* out_t, int out_levels, float v_lo, float w, int64_t nb,
                          void* table, hipStream_t stream);

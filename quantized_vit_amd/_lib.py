@@ -205,7 +205,7 @@ def gemm(A: torch.Tensor, M: int, K: int, packed: torch.Tensor, wfmt: int, N: in
 def epi_table_build(epilogue: int, out_qtype: int, out_d, out_qm, out_t, out_levels: int, v_lo: float, w: float,
                     nb: int, device: torch.device) -> torch.Tensor:
     """Code table of an int8 GEMM epilogue (qvit_epi_table_build); validity is decided on the device."""
-    table = torch.empty(16 + 8 * nb, dtype=torch.uint8, device=device)
+    table = torch.zeros((16 + 8 * nb + 1023) // 1024 * 1024, dtype=torch.uint8, device=device)  # 1-KiB pieces
     _check(load().qvit_epi_table_build(epilogue, out_qtype, _ptr(out_d), _ptr(out_qm), _ptr(out_t), out_levels,
                                        v_lo, w, nb, _ptr(table), _stream(device)), "qvit_epi_table_build")
     return table

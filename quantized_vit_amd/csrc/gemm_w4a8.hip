@@ -128,7 +128,11 @@ struct EpiTableEnt {
   int8_t lo, hi;
   int16_t pad;
 };
-constexpr int EPI_TABLE_LDS_OFF = 4 * 32 * 68 * 4;  // after the 4 waves' accumulator staging areas
+// Tables of up to TABLE_RES_NB buckets stay resident in their own LDS region, staged by LDS-DMA at kernel
+// start (before the first operand stage, so the in-order vmcnt waits of the pipeline cover them); larger
+// ones are copied into the then-idle operand ring after the main loop.
+constexpr int TABLE_RES_NB = 1536;
+constexpr int TABLE_RES_BYTES = (16 + 8 * TABLE_RES_NB + 1023) / 1024 * 1024;
 
 QVIT_DEV int epi_bucket(float v, float v_lo, float inv_w, int nb) {
   const float f = __fmul_rn(__fsub_rn(v, v_lo), inv_w);
@@ -240,7 +244,8 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   using G = Geo<WFMT, WM>;
   constexpr int BM = G::BM;
   constexpr int XBYTES = G::XBYTES;
-  __shared__ __attribute__((aligned(16))) int8_t smem[G::LDS];
+  constexpr bool I8OUT = (EPI == QVIT_EPI_I8 || EPI == QVIT_EPI_I8_GELU);
+  __shared__ __attribute__((aligned(16))) int8_t smem[G::LDS + (I8OUT ? TABLE_RES_BYTES : 0)];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -265,6 +270,17 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   // epilogue scalars are loaded before the main loop: no compiler VMEM op lands among the DMAs
   float alpha = 0.f;
   if (EPI != QVIT_EPI_I32) alpha = (*ep.d_act) * (*ep.d_wt);
+  bool use_table = false, t_resident = false;
+  float t_vlo = 0.f, t_invw = 0.f;
+  int t_nb = 1;
+  if (I8OUT && ep.table != nullptr) {
+    const EpiTableHdr h = *reinterpret_cast<const EpiTableHdr*>(ep.table);
+    use_table = h.valid != 0;
+    t_vlo = h.v_lo;
+    t_invw = h.inv_w;
+    t_nb = h.nb;
+    t_resident = use_table && t_nb <= TABLE_RES_NB;
+  }
   QVIT_STAMP_DECL
 
   // ---- LDS-DMA sources (per lane) and destinations (per wave) ---------------------------------
@@ -282,27 +298,11 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     const int logical = (lane & 3) ^ (((row >> 2) & 1) << 1);
     xsrc[j] = A + (int64_t)gm * lda + logical * 16;
   }
-  // weights: wave w stages rows [w * 256 / NWAVES, ...)
+  // weights: the packed tile of (tile_n, stage) is the LDS image itself (qvit_pack_weight), staged as
+  // contiguous 1-KiB pieces: wave w copies bytes [w * WPIECES KiB, (w + 1) * WPIECES KiB) of it
   constexpr int WROWS_PER_PIECE = 1024 / G::WROW;  // 32 (W4) or 16 (W8)
   constexpr int WROWS_PER_WAVE = BN / G::NWAVES;
-  const int64_t wrow_bytes = (WFMT == QVIT_W4) ? (int64_t)K / 2 : (int64_t)K;
-  const int8_t* wsrc[G::WPIECES];
-#pragma unroll
-  for (int j = 0; j < G::WPIECES; ++j) {
-    int row, logical;
-    if (WFMT == QVIT_W4) {
-      row = WROWS_PER_WAVE * wave + WROWS_PER_PIECE * j + (lane >> 1);
-      logical = (lane & 1) ^ ((row >> 3) & 1);
-    } else {
-      row = WROWS_PER_WAVE * wave + WROWS_PER_PIECE * j + (lane >> 2);
-      logical = (lane & 3) ^ (((row >> 2) & 1) << 1);
-    }
-#if defined(QVIT_GEMM_ABL)
-    wsrc[j] = Wp + (int64_t)((QVIT_GEMM_ABL == 5 ? 0 : n0) + row) * wrow_bytes + logical * 16;
-#else
-    wsrc[j] = Wp + (int64_t)(n0 + row) * wrow_bytes + logical * 16;
-#endif
-  }
+  const int8_t* wtile = Wp + (int64_t)tile_n * (K / BK) * G::WBYTES + wave * (G::WPIECES * 1024) + lane * 16;
   const uint32_t lds0 = lds_addr(smem);
 
   auto issue_stage = [&](int kt) {
@@ -312,26 +312,24 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     if (QVIT_GEMM_ABL == 1) return;  // no DMA
     if (QVIT_GEMM_ABL == 4) {        // contiguous 1-KiB pieces from a 128 KiB L2-hot window
       const int8_t* bx = A + (kt % 8) * 16384 + wave * 2048 + lane * 16;
-      const int8_t* bw = Wp + (kt % 8) * 8192 + wave * G::WPIECES * 1024 + lane * 16;
 #pragma unroll
       for (int j = 0; j < G::XPIECES; ++j)
         dma16(bx + j * 1024, __builtin_amdgcn_readfirstlane(sx + (32 * wave + 16 * j) * BK));
 #pragma unroll
       for (int j = 0; j < G::WPIECES; ++j)
-        dma16(bw + j * 1024,
+        dma16(Wp + (kt % 8) * G::WBYTES + wave * G::WPIECES * 1024 + lane * 16 + j * 1024,
               __builtin_amdgcn_readfirstlane(sw + (WROWS_PER_WAVE * wave + WROWS_PER_PIECE * j) * G::WROW));
       return;
     }
 #endif
     const int64_t kx = (int64_t)kt * BK;
-    const int64_t kw = (WFMT == QVIT_W4) ? kx / 2 : kx;
 #pragma unroll
     for (int j = 0; j < G::XPIECES; ++j)
       dma16(xsrc[j] + kx, __builtin_amdgcn_readfirstlane(sx + (32 * wave + 16 * j) * BK));
+    const int8_t* wt = wtile + (int64_t)kt * G::WBYTES;
 #pragma unroll
     for (int j = 0; j < G::WPIECES; ++j)
-      dma16(wsrc[j] + kw,
-            __builtin_amdgcn_readfirstlane(sw + (WROWS_PER_WAVE * wave + WROWS_PER_PIECE * j) * G::WROW));
+      dma16(wt + j * 1024, __builtin_amdgcn_readfirstlane(sw + (WROWS_PER_WAVE * wave + WROWS_PER_PIECE * j) * G::WROW));
   };
 
   // per-lane fragment offsets inside a stage
@@ -409,6 +407,11 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   using Sync0 = std::integral_constant<int, 0>;
 
   Frags<WFMT> fa, fb;
+  if (I8OUT && t_resident) {  // code table -> its LDS region (older than every stage DMA)
+    const int pieces = (16 + 8 * t_nb + 1023) / 1024;
+    for (int p = wave; p < pieces; p += G::NWAVES)
+      dma16(ep.table + p * 1024 + lane * 16, __builtin_amdgcn_readfirstlane(lds0 + G::LDS + p * 1024));
+  }
 #pragma unroll
   for (int j = 0; j < AHEAD; ++j)
     if (j < nk) issue_stage(j);
@@ -447,21 +450,58 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   if (EPI != QVIT_EPI_I32 && ep.bias != nullptr) b4 = *reinterpret_cast<const float4*>(ep.bias + n);
   if (EPI == QVIT_EPI_I8 || EPI == QVIT_EPI_I8_GELU)
     qp = load_qparams(ep.out_qtype, ep.out_d, ep.out_qm, ep.out_t, ep.out_levels);
-  // code table (if given and valid) -> LDS behind the staging areas; the flag is wave-uniform
-  bool use_table = false;
-  float t_vlo = 0.f, t_invw = 0.f;
-  int t_nb = 1;
-  const EpiTableEnt* tl = reinterpret_cast<const EpiTableEnt*>(smem + EPI_TABLE_LDS_OFF);
-  if ((EPI == QVIT_EPI_I8 || EPI == QVIT_EPI_I8_GELU) && ep.table != nullptr) {
-    const EpiTableHdr h = *reinterpret_cast<const EpiTableHdr*>(ep.table);
-    use_table = h.valid != 0;
+  if constexpr (I8OUT) {
     if (use_table) {
-      t_vlo = h.v_lo;
-      t_invw = h.inv_w;
-      t_nb = h.nb;
-      const v4i* src = reinterpret_cast<const v4i*>(ep.table + sizeof(EpiTableHdr));
-      v4i* dst = reinterpret_cast<v4i*>(smem + EPI_TABLE_LDS_OFF);
-      for (int i = tid; i < (t_nb + 1) / 2; i += G::NT) dst[i] = src[i];
+      // register epilogue: the weight-row permutation gives lane (fr, fq) the 16 consecutive columns
+      // [nbase, nbase + 16) of rows m0 + 16 s + fr, so each accumulator row leaves as one 16-B code store
+      const int8_t* tbase = smem + (t_resident ? G::LDS : 0);
+      if (!t_resident) {  // large table: into the idle operand ring
+        const v4i* src = reinterpret_cast<const v4i*>(ep.table);
+        v4i* dst = reinterpret_cast<v4i*>(smem);
+        for (int i = tid; i < (16 + 8 * t_nb + 15) / 16; i += G::NT) dst[i] = src[i];
+        __syncthreads();
+      }
+      const EpiTableEnt* tl = reinterpret_cast<const EpiTableEnt*>(tbase + sizeof(EpiTableHdr));
+      const int nbase = n0 + 64 * wn + 16 * fq;
+      float bcol[16];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ep.bias != nullptr) b = *reinterpret_cast<const float4*>(ep.bias + nbase + 4 * r);
+        bcol[4 * r] = b.x; bcol[4 * r + 1] = b.y; bcol[4 * r + 2] = b.z; bcol[4 * r + 3] = b.w;
+      }
+      const bool c16 = ((ldc & 15) == 0) && ((((uintptr_t)C) & 15) == 0);
+#pragma unroll
+      for (int sr = 0; sr < 8; ++sr) {
+        const int m = m0 + 128 * wm + 16 * sr + fr;
+        uint32_t wd[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float v = fmaf(alpha, (float)acc[r][sr][j], bcol[4 * r + j]);
+            const EpiTableEnt e = tl[epi_bucket(v, t_vlo, t_invw, t_nb)];
+            const int8_t c = v >= e.thr ? e.hi : e.lo;
+            wd[r] |= ((uint32_t)(uint8_t)c) << (8 * j);
+          }
+        if (m < M) {
+          int8_t* dst = reinterpret_cast<int8_t*>(C) + (int64_t)m * ldc + nbase;
+          if (nbase + 16 <= N) {
+            if (c16) {
+              *reinterpret_cast<uint4*>(dst) = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) reinterpret_cast<uint32_t*>(dst)[r] = wd[r];
+            }
+          } else {
+            for (int q = 0; q < 16; ++q)
+              if (nbase + q < N) dst[q] = (int8_t)((wd[q >> 2] >> (8 * (q & 3))) & 0xff);
+          }
+        }
+      }
+      QVIT_STAMP(4);
+      QVIT_STAMP_FLUSH;
+      return;
     }
   }
 
@@ -506,24 +546,6 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
           const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
           float v[4], k[4];
           bool need[4];
-          if (use_table) {
-            uint32_t word = 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const float vj = alpha * (float)a4[j] + bb[j];
-              const EpiTableEnt e = tl[epi_bucket(vj, t_vlo, t_invw, t_nb)];
-              const int8_t c = vj >= e.thr ? e.hi : e.lo;
-              word |= ((uint32_t)(uint8_t)c) << (8 * j);
-            }
-            int8_t* dst = reinterpret_cast<int8_t*>(C) + (int64_t)m * ldc + n;
-            if (nfull) {
-              *reinterpret_cast<uint32_t*>(dst) = word;
-            } else {
-              for (int j = 0; j < 4; ++j)
-                if (n + j < N) dst[j] = (int8_t)((word >> (8 * j)) & 0xff);
-            }
-            continue;
-          }
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             v[j] = alpha * (float)a4[j] + bb[j];

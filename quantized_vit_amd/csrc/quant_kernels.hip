@@ -75,6 +75,25 @@ __device__ __forceinline__ int64_t perm_row(int64_t rho) {
   return (rho & ~int64_t(63)) | (r << 4) | (q << 2) | lo;
 }
 
+// Packed weight format = the GEMM's LDS images, pre-tiled: for n-block nb (256 packed rows) and k-stage
+// st (64 k), one contiguous tile of 256 rows x 32 B (W4) / 64 B (W8); inside a tile, row r holds its 8-B
+// (W4) / 16-B (W8) chunk c at position c ^ (((r >> 3) & 1) << 1) (W4) / c ^ (((r >> 2) & 1) << 1) (W8),
+// the bank-conflict-free swizzle of the fragment reads. The GEMM stages a tile with contiguous 1-KiB
+// LDS-DMA pieces (whole cache lines). Byte offset of the 4 (W4) / 8 (W8) bytes holding k0 .. k0+7:
+template <int WFMT>
+__device__ __forceinline__ int64_t packed_offset(int64_t rho, int64_t k0, int64_t kpad) {
+  constexpr int ROWB = (WFMT == QVIT_W4) ? 32 : 64;  // bytes per row per stage
+  const int64_t nb = rho >> 8, r = rho & 255, st = k0 >> 6, kk = k0 & 63;
+  const int64_t tile = (nb * (kpad >> 6) + st) * (256 * ROWB);
+  if (WFMT == QVIT_W4) {
+    const int64_t c = kk >> 4;                                  // 8-B chunk (16 k)
+    return tile + r * ROWB + 8 * (c ^ (((r >> 3) & 1) << 1)) + ((kk & 15) >> 1);
+  } else {
+    const int64_t c = kk >> 4;                                  // 16-B chunk (16 k)
+    return tile + r * ROWB + 16 * (c ^ (((r >> 2) & 1) << 1)) + (kk & 15);
+  }
+}
+
 template <int WFMT>
 __global__ __launch_bounds__(kThreads) void pack_weight_kernel(
     const float* __restrict__ w, int64_t n, int64_t k, int64_t ldw, int qtype, const float* d,
@@ -109,7 +128,7 @@ __global__ __launch_bounds__(kThreads) void pack_weight_kernel(
         word |= ((uint32_t)(kc[b] & 0xF)) << (8 * b);
         word |= ((uint32_t)(kc[b + 4] & 0xF)) << (8 * b + 4);
       }
-      reinterpret_cast<uint32_t*>(packed)[rho * words_per_row + k0 / 8] = word;
+      *reinterpret_cast<uint32_t*>(reinterpret_cast<int8_t*>(packed) + packed_offset<QVIT_W4>(rho, k0, kpad)) = word;
     } else {
       uint32_t lo = 0, hi = 0;
 #pragma unroll
@@ -117,7 +136,7 @@ __global__ __launch_bounds__(kThreads) void pack_weight_kernel(
         lo |= ((uint32_t)(uint8_t)(int8_t)kc[b]) << (8 * b);
         hi |= ((uint32_t)(uint8_t)(int8_t)kc[b + 4]) << (8 * b);
       }
-      uint2* dst = reinterpret_cast<uint2*>(reinterpret_cast<int8_t*>(packed) + rho * kpad + k0);
+      uint2* dst = reinterpret_cast<uint2*>(reinterpret_cast<int8_t*>(packed) + packed_offset<QVIT_W8>(rho, k0, kpad));
       *dst = make_uint2(lo, hi);
     }
   }

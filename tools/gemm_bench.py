@@ -49,6 +49,12 @@ def run(name, M, N, K, epi, iters, dev, qtype=_lib.QT_NONLINEAR):
         C = torch.zeros((M, N), dtype=torch.float32, device=dev)
     d_a, d_w = p(1 / 127, dev), p(0.05 / 7, dev)
     kw = dict(out_qtype=qtype, out_d=p(4.0 / 127, dev), out_qm=p(4.0, dev), out_t=p(1.0, dev))
+    if epi in (_lib.EPI_I8, _lib.EPI_I8_GELU):
+        from quantized_vit_amd.quant_layers import epilogue_table_geometry, saturation_level
+        geo = epilogue_table_geometry(qtype, 4.0 / 127, 4.0, 1.0, saturation_level(qtype, 4.0 / 127, 4.0, 1.0),
+                                      epi == _lib.EPI_I8_GELU)
+        if geo is not None:
+            kw["epi_table"] = _lib.epi_table_build(epi, qtype, kw["out_d"], kw["out_qm"], kw["out_t"], 0, *geo, dev)
     times = []
     for i in range(iters + 3):
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
