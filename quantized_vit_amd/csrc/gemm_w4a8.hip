@@ -92,6 +92,12 @@ QVIT_DEV void dma16(const void* gsrc, uint32_t lds_base) {
 template <int N>
 QVIT_DEV void stage_sync() {
   __builtin_amdgcn_s_waitcnt(0xC07F);
+#if defined(QVIT_GEMM_ABL)
+  if (QVIT_GEMM_ABL == 8) {  // diagnostic: no barrier (valid only with a static LDS image)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+    return;
+  }
+#endif
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
@@ -131,7 +137,7 @@ struct EpiTableEnt {
 // Tables of up to TABLE_RES_NB buckets stay resident in their own LDS region, staged by LDS-DMA at kernel
 // start (before the first operand stage, so the in-order vmcnt waits of the pipeline cover them); larger
 // ones are copied into the then-idle operand ring after the main loop.
-constexpr int TABLE_RES_NB = 1536;
+constexpr int TABLE_RES_NB = 0;
 constexpr int TABLE_RES_BYTES = (16 + 8 * TABLE_RES_NB + 1023) / 1024 * 1024;
 
 QVIT_DEV int epi_bucket(float v, float v_lo, float inv_w, int nb) {
@@ -245,7 +251,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   constexpr int BM = G::BM;
   constexpr int XBYTES = G::XBYTES;
   constexpr bool I8OUT = (EPI == QVIT_EPI_I8 || EPI == QVIT_EPI_I8_GELU);
-  __shared__ __attribute__((aligned(16))) int8_t smem[G::LDS + (I8OUT ? TABLE_RES_BYTES : 0)];
+  __shared__ __attribute__((aligned(16))) int8_t smem[G::LDS + ((I8OUT && TABLE_RES_NB > 0) ? TABLE_RES_BYTES : 0)];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -309,7 +315,8 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     const uint32_t sx = lds0 + (uint32_t)((kt % RING) * G::STAGE);
     const uint32_t sw = sx + XBYTES;
 #if defined(QVIT_GEMM_ABL)  // diagnostic builds only (tools/gemm_stamps.py --abl): wrong results
-    if (QVIT_GEMM_ABL == 1) return;  // no DMA
+    if (QVIT_GEMM_ABL == 1) return;                  // no DMA
+    if ((QVIT_GEMM_ABL == 6 || QVIT_GEMM_ABL == 7 || QVIT_GEMM_ABL == 8) && kt >= AHEAD) return;  // prologue only
     if (QVIT_GEMM_ABL == 4) {        // contiguous 1-KiB pieces from a 128 KiB L2-hot window
       const int8_t* bx = A + (kt % 8) * 16384 + wave * 2048 + lane * 16;
 #pragma unroll
@@ -363,6 +370,11 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
       v4i wf;
       if (WFMT == QVIT_W4) {
         const uint2 p = f.w4[r];
+#if defined(QVIT_GEMM_ABL)
+        if (QVIT_GEMM_ABL == 7) {  // diagnostic: no int4 -> int8 unpack
+          wf = v4i{(int)p.x, (int)p.y, (int)p.x, (int)p.y};
+        } else
+#endif
         wf = v4i{(int)sext4_lo(p.x), (int)sext4_hi(p.x), (int)sext4_lo(p.y), (int)sext4_hi(p.y)};
       } else {
         wf = f.w8[r];
@@ -437,6 +449,17 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
+#if defined(QVIT_GEMM_ABL)
+  if (QVIT_GEMM_ABL >= 6) {  // diagnostic: no epilogue (accumulators folded into one store per lane)
+    int x = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int sr = 0; sr < 8; ++sr) x ^= acc[r][sr][0] ^ acc[r][sr][1] ^ acc[r][sr][2] ^ acc[r][sr][3];
+    if (x == 0x7fffffff) reinterpret_cast<int*>(C)[tid] = x;
+    return;
+  }
+#endif
   // ---- epilogue ---------------------------------------------------------------------------------
   // acc[r][s][j] = C[m0 + 128 wm + 16 s + fr][n0 + 64 wn + 16 fq + 4 r + j] (weight rows pre-permuted)
   int* stg = reinterpret_cast<int*>(smem) + wave * EPI_WAVE_INTS;

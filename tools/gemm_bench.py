@@ -27,6 +27,7 @@ SHAPES = {
     "fc1_f32": (M_B256, 3072, 768, _lib.EPI_F32),
     "fc1_i32": (M_B256, 3072, 768, _lib.EPI_I32),
     "fc1_i8": (M_B256, 3072, 768, _lib.EPI_I8),
+    "fc1_i8nt": (M_B256, 3072, 768, _lib.EPI_I8),   # no code table: per-element quantizer
     "fc2": (M_B256, 768, 3072, _lib.EPI_F32_RESID),
     "big": (16384, 8192, 4096, _lib.EPI_I32),
 }
@@ -49,7 +50,7 @@ def run(name, M, N, K, epi, iters, dev, qtype=_lib.QT_NONLINEAR):
         C = torch.zeros((M, N), dtype=torch.float32, device=dev)
     d_a, d_w = p(1 / 127, dev), p(0.05 / 7, dev)
     kw = dict(out_qtype=qtype, out_d=p(4.0 / 127, dev), out_qm=p(4.0, dev), out_t=p(1.0, dev))
-    if epi in (_lib.EPI_I8, _lib.EPI_I8_GELU):
+    if epi in (_lib.EPI_I8, _lib.EPI_I8_GELU) and not name.endswith("nt"):
         from quantized_vit_amd.quant_layers import epilogue_table_geometry, saturation_level
         geo = epilogue_table_geometry(qtype, 4.0 / 127, 4.0, 1.0, saturation_level(qtype, 4.0 / 127, 4.0, 1.0),
                                       epi == _lib.EPI_I8_GELU)
