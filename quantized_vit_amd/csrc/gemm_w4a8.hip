@@ -32,30 +32,38 @@ namespace {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 
-constexpr int BN = 256;    // weight rows per block
+constexpr int BN = 256;    // weight rows per tile
 constexpr int BK = 64;     // k per stage
 constexpr int KTILE = 128; // the API's K granularity (QVIT_TILE_K): stages come in pairs
-constexpr int RING = 4;    // LDS stages
-constexpr int AHEAD = 3;   // stages in flight ahead of the one being computed
+constexpr int RING = 3;    // LDS stages
+// stages in flight ahead of the one being computed: 2 (the tail steps of a tile issue the next
+// tile's stages 0 and 1; the steady steps issue stage kt + 2)
 constexpr int EPI_LD = 68; // staged accumulator row pitch (ints): 64 + 4 pad
-constexpr int EPI_WAVE_INTS = 32 * EPI_LD;
+constexpr int EPI_ROWS = 16;                            // rows staged per pass per wave
+constexpr int EPI_WAVE_BYTES = EPI_ROWS * EPI_LD * 4;   // 4352
 
-// WM = waves along m: WM = 1 -> 4 waves, tile 256 (n) x 128 (m), 2 blocks / CU;
-//                     WM = 2 -> 8 waves, tile 256 (n) x 256 (m), 1 block / CU (half the bytes per op)
+// WM = waves along m: WM = 1 -> 4 waves, tile 256 (n) x 128 (m). The LDS holds the operand ring and a
+// separate epilogue region (accumulator staging, or the int8 code table), so a block's epilogue never
+// touches the ring and the DMA of its next tile's first stages proceeds underneath it.
 template <int WFMT, int WM>
 struct Geo {
   static constexpr int NT = 256 * WM;
   static constexpr int NWAVES = 4 * WM;
   static constexpr int BM = 128 * WM;
-  static constexpr int XBYTES = BM * BK;                        // 8 / 16 KiB activation tile per stage
+  static constexpr int XBYTES = BM * BK;                        // 8 KiB activation tile per stage
   static constexpr int WROW = (WFMT == QVIT_W4) ? BK / 2 : BK;  // bytes per weight row per stage
   static constexpr int WBYTES = BN * WROW;                      // 8 KiB (W4) / 16 KiB (W8)
   static constexpr int STAGE = XBYTES + WBYTES;
-  static constexpr int LDS = RING * STAGE;
+  static constexpr int RING_BYTES = RING * STAGE;
+  static constexpr int EPI_BYTES = NWAVES * EPI_WAVE_BYTES;     // 17 KiB: staging, or a table of <= 2174 buckets
+  static constexpr int BIAS_BYTES = BN * 4;                     // the tile's bias, DMA'd at its head
+  static constexpr int QP_BYTES = 64;                           // the output quantizer's scalars
+  static constexpr int LDS = RING_BYTES + EPI_BYTES + BIAS_BYTES + QP_BYTES;
   static constexpr int XPIECES = XBYTES / 1024 / NWAVES;        // 1-KiB DMA pieces per wave
   static constexpr int WPIECES = WBYTES / 1024 / NWAVES;
   static constexpr int DMA_PER_STAGE = XPIECES + WPIECES;       // per wave
   static constexpr int MIN_BLOCKS = (WFMT == QVIT_W4 && WM == 1) ? 2 : 1;
+  static constexpr int TABLE_MAX_NB = (EPI_BYTES - 16) / 8;
 };
 
 QVIT_DEV uint32_t sext4_lo(uint32_t p) {
@@ -65,6 +73,14 @@ QVIT_DEV uint32_t sext4_lo(uint32_t p) {
 QVIT_DEV uint32_t sext4_hi(uint32_t p) {
   const uint32_t x = (p >> 4) & 0x0F0F0F0Fu;
   return ((x ^ 0x08080808u) + 0x78787878u) ^ 0x80808080u;
+}
+
+// Lane id from a volatile asm: values derived from it are recomputed where used instead of being
+// hoisted out of the tile loop (which would keep them live across the register-bound main loop).
+QVIT_DEV int lane_opaque() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
 }
 
 QVIT_DEV uint32_t lds_addr(const void* p) {
@@ -134,12 +150,6 @@ struct EpiTableEnt {
   int8_t lo, hi;
   int16_t pad;
 };
-// Tables of up to TABLE_RES_NB buckets stay resident in their own LDS region, staged by LDS-DMA at kernel
-// start (before the first operand stage, so the in-order vmcnt waits of the pipeline cover them); larger
-// ones are copied into the then-idle operand ring after the main loop.
-constexpr int TABLE_RES_NB = 0;
-constexpr int TABLE_RES_BYTES = (16 + 8 * TABLE_RES_NB + 1023) / 1024 * 1024;
-
 QVIT_DEV int epi_bucket(float v, float v_lo, float inv_w, int nb) {
   const float f = __fmul_rn(__fsub_rn(v, v_lo), inv_w);
   return (int)fminf(fmaxf(f, 0.f), (float)(nb - 1));  // NaN -> 0
@@ -240,10 +250,12 @@ struct Frags {
   v4i w8[4];    // W8: 16 bytes per lane
 };
 
-// SHORT: K == 128 (two stages, all issued by the prologue); separate so that the steady-state
-// kernel has a single static tail (a runtime choice between tails makes the accumulators PHIs and
-// the register allocator then copies and spills them).
-template <int WFMT, int EPI, int WM, bool SHORT>
+// Persistent kernel: gridDim.x = a multiple of 8 (blocks are dispatched round-robin over the 8 XCDs);
+// XCD x's blocks share the contiguous tile range [lo_x, hi_x) (tile_n fastest, so the tiles in flight on
+// one XCD share their activation panels in its L2), block slot s of the XCD walks lo_x + s + i * team.
+// The operand stages form one stream across the block's tiles: the last two steps of a tile issue the
+// DMA of the next tile's first two stages, so the pipeline never drains between tiles.
+template <int WFMT, int EPI, int WM>
 __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) void gemm_kernel(
     const int8_t* __restrict__ A, int M, int K, int64_t lda, const int8_t* __restrict__ Wp, int N, int npad,
     void* __restrict__ C, int64_t ldc, EpiArgs ep) {
@@ -251,7 +263,11 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   constexpr int BM = G::BM;
   constexpr int XBYTES = G::XBYTES;
   constexpr bool I8OUT = (EPI == QVIT_EPI_I8 || EPI == QVIT_EPI_I8_GELU);
-  __shared__ __attribute__((aligned(16))) int8_t smem[G::LDS + ((I8OUT && TABLE_RES_NB > 0) ? TABLE_RES_BYTES : 0)];
+  __shared__ __attribute__((aligned(16))) int8_t smem[G::LDS];
+  int8_t* epi_lds = smem + G::RING_BYTES;
+  const float* bias_l = reinterpret_cast<const float*>(smem + G::RING_BYTES + G::EPI_BYTES);
+  QParams* qp_l = reinterpret_cast<QParams*>(smem + G::RING_BYTES + G::EPI_BYTES + G::BIAS_BYTES);
+  const bool has_bias = (EPI != QVIT_EPI_I32) && ep.bias != nullptr;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -261,79 +277,70 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   const int fr = lane & 15;
   const int fq = lane >> 4;
 
-  // ---- tile assignment with a bijective XCD remap ----------------------------------------
+  // ---- this block's tiles ---------------------------------------------------------------------
   const int nb_n = npad / BN;
-  const int nb_m = (M + BM - 1) / BM;
-  const int nblk = nb_n * nb_m;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nblk >> 3, r8 = nblk & 7;
-  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int tile_n = lid % nb_n;
-  const int tile_m = lid / nb_n;
-  const int n0 = tile_n * BN;
-  const int m0 = tile_m * BM;
+  const int ntiles = nb_n * ((M + BM - 1) / BM);
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, team = gridDim.x >> 3;
+  const int per = ntiles >> 3, rem = ntiles & 7;
+  const int lo = xcd * per + (xcd < rem ? xcd : rem);
+  const int hi = lo + per + (xcd < rem ? 1 : 0);
+  int t = lo + slot;
+  if (t >= hi) return;
 
-  // epilogue scalars are loaded before the main loop: no compiler VMEM op lands among the DMAs
+  // epilogue scalars and the code table are set up before the main loop
   float alpha = 0.f;
   if (EPI != QVIT_EPI_I32) alpha = (*ep.d_act) * (*ep.d_wt);
-  bool use_table = false, t_resident = false;
+  bool use_table = false;
   float t_vlo = 0.f, t_invw = 0.f;
   int t_nb = 1;
   if (I8OUT && ep.table != nullptr) {
     const EpiTableHdr h = *reinterpret_cast<const EpiTableHdr*>(ep.table);
-    use_table = h.valid != 0;
+    use_table = h.valid != 0 && h.nb <= G::TABLE_MAX_NB;
     t_vlo = h.v_lo;
     t_invw = h.inv_w;
     t_nb = h.nb;
-    t_resident = use_table && t_nb <= TABLE_RES_NB;
-  }
-  QVIT_STAMP_DECL
-
-  // ---- LDS-DMA sources (per lane) and destinations (per wave) ---------------------------------
-  // activations: wave w stages rows [32w, 32w+32) as 2 pieces of 16 rows x 64 B
-  const int8_t* xsrc[G::XPIECES];
-#pragma unroll
-  for (int j = 0; j < G::XPIECES; ++j) {
-    const int row = 32 * wave + 16 * j + (lane >> 2);
-#if defined(QVIT_GEMM_ABL)
-    int gm = (QVIT_GEMM_ABL == 5 ? 0 : m0) + row;
-#else
-    int gm = m0 + row;
-#endif
-    gm = gm < M ? gm : M - 1;  // clamp the tail: staged, never stored
-    const int logical = (lane & 3) ^ (((row >> 2) & 1) << 1);
-    xsrc[j] = A + (int64_t)gm * lda + logical * 16;
-  }
-  // weights: the packed tile of (tile_n, stage) is the LDS image itself (qvit_pack_weight), staged as
-  // contiguous 1-KiB pieces: wave w copies bytes [w * WPIECES KiB, (w + 1) * WPIECES KiB) of it
-  constexpr int WROWS_PER_PIECE = 1024 / G::WROW;  // 32 (W4) or 16 (W8)
-  constexpr int WROWS_PER_WAVE = BN / G::NWAVES;
-  const int8_t* wtile = Wp + (int64_t)tile_n * (K / BK) * G::WBYTES + wave * (G::WPIECES * 1024) + lane * 16;
-  const uint32_t lds0 = lds_addr(smem);
-
-  auto issue_stage = [&](int kt) {
-    const uint32_t sx = lds0 + (uint32_t)((kt % RING) * G::STAGE);
-    const uint32_t sw = sx + XBYTES;
-#if defined(QVIT_GEMM_ABL)  // diagnostic builds only (tools/gemm_stamps.py --abl): wrong results
-    if (QVIT_GEMM_ABL == 1) return;                  // no DMA
-    if ((QVIT_GEMM_ABL == 6 || QVIT_GEMM_ABL == 7 || QVIT_GEMM_ABL == 8) && kt >= AHEAD) return;  // prologue only
-    if (QVIT_GEMM_ABL == 4) {        // contiguous 1-KiB pieces from a 128 KiB L2-hot window
-      const int8_t* bx = A + (kt % 8) * 16384 + wave * 2048 + lane * 16;
-#pragma unroll
-      for (int j = 0; j < G::XPIECES; ++j)
-        dma16(bx + j * 1024, __builtin_amdgcn_readfirstlane(sx + (32 * wave + 16 * j) * BK));
-#pragma unroll
-      for (int j = 0; j < G::WPIECES; ++j)
-        dma16(Wp + (kt % 8) * G::WBYTES + wave * G::WPIECES * 1024 + lane * 16 + j * 1024,
-              __builtin_amdgcn_readfirstlane(sw + (WROWS_PER_WAVE * wave + WROWS_PER_PIECE * j) * G::WROW));
-      return;
+    if (use_table) {  // -> the epilogue region, once per block (made visible by the first stage sync)
+      const v4i* src = reinterpret_cast<const v4i*>(ep.table);
+      for (int i = tid; i < (16 + 8 * t_nb + 15) / 16; i += G::NT) reinterpret_cast<v4i*>(epi_lds)[i] = src[i];
     }
+  }
+  // the direct quantizer's scalars: derived once (double-precision exp/log) and kept in LDS, so
+  // nothing of it stays live across the main loop
+  if (I8OUT && !use_table && tid == 0) *qp_l = load_qparams(ep.out_qtype, ep.out_d, ep.out_qm, ep.out_t, ep.out_levels);
+
+  // ---- LDS-DMA sources (per lane) of a tile -----------------------------------------------------
+  // activations: wave w stages rows [32w, 32w+32) as 2 pieces of 16 rows x 64 B (swizzle on the source)
+  // weights: the packed (tile_n, stage) tile is the LDS image itself, staged as contiguous 1-KiB pieces
+  constexpr int WROWS_PER_PIECE = 1024 / G::WROW;
+  constexpr int WROWS_PER_WAVE = BN / G::NWAVES;
+  const int nk = K / BK;  // even, >= 2
+  // a tile's sources are uniform (m0, weight-tile base); the per-lane parts are tile-invariant
+  struct Src {
+    int m0;
+    const int8_t* w;
+  };
+  auto tile_src = [&](int tt, Src& sr) {
+    sr.m0 = (tt / nb_n) * BM;
+    sr.w = Wp + (int64_t)(tt % nb_n) * nk * G::WBYTES;
+  };
+  const uint32_t lds0 = lds_addr(smem);
+  auto issue = [&](const Src& sr, int kt, int rslot) {
+#if defined(QVIT_GEMM_ABL)
+    if (QVIT_GEMM_ABL == 1) return;  // diagnostic: no DMA
 #endif
+    const uint32_t sx = lds0 + (uint32_t)(rslot * G::STAGE);
+    const uint32_t sw = sx + XBYTES;
     const int64_t kx = (int64_t)kt * BK;
+    const int lane_now = lane_opaque();
 #pragma unroll
-    for (int j = 0; j < G::XPIECES; ++j)
-      dma16(xsrc[j] + kx, __builtin_amdgcn_readfirstlane(sx + (32 * wave + 16 * j) * BK));
-    const int8_t* wt = wtile + (int64_t)kt * G::WBYTES;
+    for (int j = 0; j < G::XPIECES; ++j) {
+      const int row = 32 * wave + 16 * j + (lane_now >> 2);
+      int gm = sr.m0 + row;
+      gm = gm < M ? gm : M - 1;  // clamp the tail: staged, never stored
+      const int lg = ((lane_now & 3) ^ (((row >> 2) & 1) << 1)) * 16;
+      dma16(A + (int64_t)gm * lda + lg + kx, __builtin_amdgcn_readfirstlane(sx + (32 * wave + 16 * j) * BK));
+    }
+    const int8_t* wt = sr.w + (int64_t)kt * G::WBYTES + wave * (G::WPIECES * 1024) + lane_now * 16;
 #pragma unroll
     for (int j = 0; j < G::WPIECES; ++j)
       dma16(wt + j * 1024, __builtin_amdgcn_readfirstlane(sw + (WROWS_PER_WAVE * wave + WROWS_PER_PIECE * j) * G::WROW));
@@ -343,9 +350,8 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   const int xoff = (128 * wm + fr) * BK + ((fq ^ (((fr >> 2) & 1) << 1)) << 4);
   const int woff = (WFMT == QVIT_W4) ? (64 * wn + fr) * G::WROW + ((fq ^ (((fr >> 3) & 1) << 1)) << 3)
                                      : (64 * wn + fr) * G::WROW + ((fq ^ (((fr >> 2) & 1) << 1)) << 4);
-
-  auto read_frags = [&](int kt, Frags<WFMT>& f) {
-    const int8_t* sx = smem + (kt % RING) * G::STAGE;
+  auto read_frags = [&](int rslot, Frags<WFMT>& f) {
+    const int8_t* sx = smem + rslot * G::STAGE;
     const int8_t* sw = sx + XBYTES;
 #pragma unroll
     for (int s = 0; s < 8; ++s) f.x[s] = *reinterpret_cast<const v4i*>(sx + xoff + s * 16 * BK);
@@ -359,22 +365,12 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   };
 
   v4i acc[4][8];
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int s = 0; s < 8; ++s) acc[r][s] = v4i{0, 0, 0, 0};
-
   auto mfma_stage = [&](const Frags<WFMT>& f) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       v4i wf;
       if (WFMT == QVIT_W4) {
         const uint2 p = f.w4[r];
-#if defined(QVIT_GEMM_ABL)
-        if (QVIT_GEMM_ABL == 7) {  // diagnostic: no int4 -> int8 unpack
-          wf = v4i{(int)p.x, (int)p.y, (int)p.x, (int)p.y};
-        } else
-#endif
         wf = v4i{(int)sext4_lo(p.x), (int)sext4_hi(p.x), (int)sext4_lo(p.y), (int)sext4_hi(p.y)};
       } else {
         wf = f.w8[r];
@@ -385,118 +381,101 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   };
 
   // One pipeline step: stage kt is in registers (cur); bring stage kt+1 into registers (nxt).
-  // ISSUE: DMA stage kt+AHEAD; SYNC: this wave's DMAs allowed in flight when stage kt+1 is read
-  // (the stages newer than kt+1); READ: there is a stage kt+1. All three are compile-time per call
-  // site so the steady-state loop carries no branches: a join after conditional fragment reads makes
-  // the compiler drain lgkmcnt(0) in front of the MFMAs, serialising LDS latency with every stage.
+  // The phases are fenced (sched_barrier) and the LDS drain at the top is compiler-visible, so the
+  // fragment reads of stage kt+1 overlap the MFMAs of stage kt with no wait between them.
   constexpr int D = G::DMA_PER_STAGE;
-  const int nk = K / BK;  // even: K is a multiple of KTILE
-  auto step = [&](int kt, Frags<WFMT>& cur, Frags<WFMT>& nxt, auto issue, auto sync, auto read)
-                  __attribute__((always_inline)) {
-    // cur's fragment reads were issued a full stage of MFMAs ago; retiring them where the compiler
-    // can see it keeps the wait-count model exact at the MFMAs below.
-    // sched_barrier(0) fences keep the phases in this order: the steady loop is one basic block and
-    // the scheduler otherwise hoists nxt's unpack up to its reads (forcing a wait) across steps.
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    QVIT_STAMP(5);
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (decltype(issue)::value) issue_stage(kt + AHEAD);
-    QVIT_STAMP(1);
-    if constexpr (decltype(read)::value) {
-      stage_sync<decltype(sync)::value>();
-      QVIT_STAMP(2);
-      read_frags(kt + 1, nxt);
-    }
+  auto step_core = [&](Frags<WFMT>& cur, Frags<WFMT>& nxt, int next_slot, bool read) __attribute__((always_inline)) {
+    if (read) read_frags(next_slot, nxt);
     __builtin_amdgcn_sched_barrier(0);
     mfma_stage(cur);
     __builtin_amdgcn_sched_barrier(0);
-    QVIT_STAMP(3);
   };
-  using Yes = std::true_type;
-  using No = std::false_type;
-  using Sync2 = std::integral_constant<int, 2 * D>;
-  using Sync1 = std::integral_constant<int, D>;
-  using Sync0 = std::integral_constant<int, 0>;
 
+  Src cs, ns;
+  tile_src(t, cs);
+  // prologue: the first tile's stages 0 and 1
+  int g = 0;  // global stage counter of this block (ring slot = g % RING)
+  issue(cs, 0, 0);
+  issue(cs, 1, 1);
   Frags<WFMT> fa, fb;
-  if (I8OUT && t_resident) {  // code table -> its LDS region (older than every stage DMA)
-    const int pieces = (16 + 8 * t_nb + 1023) / 1024;
-    for (int p = wave; p < pieces; p += G::NWAVES)
-      dma16(ep.table + p * 1024 + lane * 16, __builtin_amdgcn_readfirstlane(lds0 + G::LDS + p * 1024));
-  }
-#pragma unroll
-  for (int j = 0; j < AHEAD; ++j)
-    if (j < nk) issue_stage(j);
-  if (nk > 2) stage_sync<2 * D>();
-  else stage_sync<D>();
-  read_frags(0, fa);
-  QVIT_STAMP(0);
-  int kt = 0;
-  if constexpr (!SHORT)
-  for (; kt + 5 <= nk; kt += 2) {  // both steps issue, two newer stages in flight
-    step(kt, fa, fb, Yes{}, Sync2{}, Yes{});
-    step(kt + 1, fb, fa, Yes{}, Sync2{}, Yes{});
-  }
-  if constexpr (!SHORT) {  // kt == nk - 4
-    step(kt, fa, fb, Yes{}, Sync2{}, Yes{});
-    step(kt + 1, fb, fa, No{}, Sync1{}, Yes{});
-    step(kt + 2, fa, fb, No{}, Sync0{}, Yes{});
-    step(kt + 3, fb, fa, No{}, Sync0{}, No{});
-  } else {  // nk == 2: both stages were issued by the prologue
-    step(0, fa, fb, No{}, Sync0{}, Yes{});
-    step(1, fb, fa, No{}, Sync0{}, No{});
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-#if defined(QVIT_GEMM_ABL)
-  if (QVIT_GEMM_ABL >= 6) {  // diagnostic: no epilogue (accumulators folded into one store per lane)
-    int x = 0;
+  for (;;) {
+    const int tnext = t + team;
+    const bool has_next = tnext < hi;
+    if (has_next) tile_src(tnext, ns);
+    const int m0 = (t / nb_n) * BM, n0 = (t % nb_n) * BN;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int sr = 0; sr < 8; ++sr) x ^= acc[r][sr][0] ^ acc[r][sr][1] ^ acc[r][sr][2] ^ acc[r][sr][3];
-    if (x == 0x7fffffff) reinterpret_cast<int*>(C)[tid] = x;
-    return;
-  }
-#endif
-  // ---- epilogue ---------------------------------------------------------------------------------
-  // acc[r][s][j] = C[m0 + 128 wm + 16 s + fr][n0 + 64 wn + 16 fq + 4 r + j] (weight rows pre-permuted)
-  int* stg = reinterpret_cast<int*>(smem) + wave * EPI_WAVE_INTS;
-  const int prow = lane >> 4;        // processing: row 4 i + prow of the staged 32
-  const int pcol = 4 * (lane & 15);  // 4 consecutive columns of the wave's 64
-  const int n = n0 + 64 * wn + pcol;
-  const bool nfull = n + 4 <= N;
+      for (int s = 0; s < 8; ++s) acc[r][s] = v4i{0, 0, 0, 0};
 
-  float4 b4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  QParams qp;
-  if (EPI != QVIT_EPI_I32 && ep.bias != nullptr) b4 = *reinterpret_cast<const float4*>(ep.bias + n);
-  if (EPI == QVIT_EPI_I8 || EPI == QVIT_EPI_I8_GELU)
-    qp = load_qparams(ep.out_qtype, ep.out_d, ep.out_qm, ep.out_t, ep.out_levels);
-  if constexpr (I8OUT) {
-    if (use_table) {
-      // register epilogue: the weight-row permutation gives lane (fr, fq) the 16 consecutive columns
-      // [nbase, nbase + 16) of rows m0 + 16 s + fr, so each accumulator row leaves as one 16-B code store
-      const int8_t* tbase = smem + (t_resident ? G::LDS : 0);
-      if (!t_resident) {  // large table: into the idle operand ring
-        const v4i* src = reinterpret_cast<const v4i*>(ep.table);
-        v4i* dst = reinterpret_cast<v4i*>(smem);
-        for (int i = tid; i < (16 + 8 * t_nb + 15) / 16; i += G::NT) dst[i] = src[i];
-        __syncthreads();
-      }
-      const EpiTableEnt* tl = reinterpret_cast<const EpiTableEnt*>(tbase + sizeof(EpiTableHdr));
-      const int nbase = n0 + 64 * wn + 16 * fq;
+    // head: stage 0 of this tile landed (stage 1 may still be in flight); every wave is past the
+    // previous tile's epilogue, so the tile's bias can be DMA'd into its LDS slot (1 KiB, wave 0;
+    // older than every later stage DMA, so the counted stage waits cover it)
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    stage_sync<D>();
+    if (has_bias && wave == 0)
+      dma16(ep.bias + n0 + lane_opaque() * 4, __builtin_amdgcn_readfirstlane(lds0 + G::RING_BYTES + G::EPI_BYTES));
+    read_frags(g % RING, fa);
+    // steady steps kt = 0 .. nk-3: issue this tile's stage kt+2
+    int kt = 0;
+    for (; kt < nk - 2; kt += 2) {
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_sched_barrier(0);
+      issue(cs, kt + 2, (g + kt + 2) % RING);
+      stage_sync<D>();
+      step_core(fa, fb, (g + kt + 1) % RING, true);
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_sched_barrier(0);
+      issue(cs, kt + 3, (g + kt + 3) % RING);
+      stage_sync<D>();
+      step_core(fb, fa, (g + kt + 2) % RING, true);
+    }
+    // tail kt = nk-2, nk-1: issue the next tile's stages 0, 1
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_sched_barrier(0);
+    if (has_next) {
+      issue(ns, 0, (g + nk) % RING);
+      stage_sync<D>();
+    } else {
+      stage_sync<0>();
+    }
+    step_core(fa, fb, (g + nk - 1) % RING, true);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_sched_barrier(0);
+    if (has_next) issue(ns, 1, (g + nk + 1) % RING);
+    step_core(fb, fa, 0, false);
+
+#if defined(QVIT_GEMM_ABL)
+    if (QVIT_GEMM_ABL == 6) {  // diagnostic: no epilogue (accumulators folded into one store per lane)
+      int x = 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int sr = 0; sr < 8; ++sr) x ^= acc[r][sr][0] ^ acc[r][sr][1] ^ acc[r][sr][2] ^ acc[r][sr][3];
+      if (x == 0x7fffffff) reinterpret_cast<int*>(C)[tid] = x;
+    } else
+#endif
+    {
+    // ---- epilogue (epilogue LDS region only; the next tile's DMA streams underneath) -----------
+    // acc[r][s][j] = C[m0 + 128 wm + 16 s + fr][n0 + 64 wn + 16 fq + 4 r + j] (weight rows pre-permuted)
+    const int el = lane_opaque();
+    const int efr = el & 15, efq = el >> 4;
+    if (I8OUT && use_table) {
+      // register path: lane (fr, fq) owns the 16 consecutive columns [nbase, nbase+16) of rows
+      // m0 + 16 s + fr, so each accumulator row leaves as one 16-B code store
+      const EpiTableEnt* tl = reinterpret_cast<const EpiTableEnt*>(epi_lds + sizeof(EpiTableHdr));
+      const int nbase = n0 + 64 * wn + 16 * efq;
       float bcol[16];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (ep.bias != nullptr) b = *reinterpret_cast<const float4*>(ep.bias + nbase + 4 * r);
+        if (has_bias) b = *reinterpret_cast<const float4*>(bias_l + (nbase - n0) + 4 * r);
         bcol[4 * r] = b.x; bcol[4 * r + 1] = b.y; bcol[4 * r + 2] = b.z; bcol[4 * r + 3] = b.w;
       }
       const bool c16 = ((ldc & 15) == 0) && ((((uintptr_t)C) & 15) == 0);
 #pragma unroll
       for (int sr = 0; sr < 8; ++sr) {
-        const int m = m0 + 128 * wm + 16 * sr + fr;
+        const int m = m0 + 128 * wm + 16 * sr + efr;
         uint32_t wd[4] = {0, 0, 0, 0};
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -522,95 +501,117 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
           }
         }
       }
-      QVIT_STAMP(4);
-      QVIT_STAMP_FLUSH;
-      return;
-    }
-  }
-
+    } else {
+      // staged path: 16 accumulator rows at a time through this wave's own staging area, then 16 lanes
+      // own one contiguous 64-column row segment (256-B fp32 rows / 64-B code rows); wave-local only
+      int* stg = reinterpret_cast<int*>(epi_lds + wave * EPI_WAVE_BYTES);
+      const int prow = el >> 4;          // row 4 i + prow of the staged 16
+      const int pcol = 4 * (el & 15);    // 4 consecutive columns of the wave's 64
+      const int n = n0 + 64 * wn + pcol;
+      const bool nfull = n + 4 <= N;
+      float4 b4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (has_bias) b4 = *reinterpret_cast<const float4*>(bias_l + (n - n0));
+      QParams qp;
+      if (I8OUT) qp = *qp_l;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+      for (int sr = 0; sr < 8; ++sr) {
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // the previous pass's staged reads are done
 #pragma unroll
-    for (int sl = 0; sl < 2; ++sl)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        *reinterpret_cast<v4i*>(stg + (16 * sl + fr) * EPI_LD + 16 * fq + 4 * r) = acc[r][2 * q + sl];
-    __syncthreads();
+        for (int r = 0; r < 4; ++r)
+          *reinterpret_cast<v4i*>(stg + efr * EPI_LD + 16 * efq + 4 * r) = acc[r][sr];
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll 1
-    for (int i = 0; i < 8; ++i) {
-      const int row = 4 * i + prow;
-      const int m = m0 + 128 * wm + 32 * q + row;
-      const v4i a4 = *reinterpret_cast<const v4i*>(stg + row * EPI_LD + pcol);
-      if (m < M) {
-        if (EPI == QVIT_EPI_I32) {
-          int32_t* dst = reinterpret_cast<int32_t*>(C) + (int64_t)m * ldc + n;
-          if (nfull) {
-            *reinterpret_cast<v4i*>(dst) = a4;
-          } else {
-            for (int j = 0; j < 4; ++j)
-              if (n + j < N) dst[j] = a4[j];
-          }
-        } else if (EPI == QVIT_EPI_F32 || EPI == QVIT_EPI_F32_RESID) {
-          float4 o = make_float4(alpha * (float)a4[0] + b4.x, alpha * (float)a4[1] + b4.y,
-                                 alpha * (float)a4[2] + b4.z, alpha * (float)a4[3] + b4.w);
-          float* dst = reinterpret_cast<float*>(C) + (int64_t)m * ldc + n;
-          if (nfull) {
-            if (EPI == QVIT_EPI_F32_RESID) {
-              const float4 old = *reinterpret_cast<const float4*>(dst);
-              o.x += old.x; o.y += old.y; o.z += old.z; o.w += old.w;
+        for (int i = 0; i < 4; ++i) {
+          const int row = 4 * i + prow;
+          const int m = m0 + 128 * wm + 16 * sr + row;
+          const v4i a4 = *reinterpret_cast<const v4i*>(stg + row * EPI_LD + pcol);
+          if (m < M) {
+            if (EPI == QVIT_EPI_I32) {
+              int32_t* dst = reinterpret_cast<int32_t*>(C) + (int64_t)m * ldc + n;
+              if (nfull) {
+                *reinterpret_cast<v4i*>(dst) = a4;
+              } else {
+                for (int j = 0; j < 4; ++j)
+                  if (n + j < N) dst[j] = a4[j];
+              }
+            } else if (EPI == QVIT_EPI_F32 || EPI == QVIT_EPI_F32_RESID) {
+              float4 o = make_float4(alpha * (float)a4[0] + b4.x, alpha * (float)a4[1] + b4.y,
+                                     alpha * (float)a4[2] + b4.z, alpha * (float)a4[3] + b4.w);
+              float* dst = reinterpret_cast<float*>(C) + (int64_t)m * ldc + n;
+              if (nfull) {
+                if (EPI == QVIT_EPI_F32_RESID) {
+                  const float4 old = *reinterpret_cast<const float4*>(dst);
+                  o.x += old.x; o.y += old.y; o.z += old.z; o.w += old.w;
+                }
+                *reinterpret_cast<float4*>(dst) = o;
+              } else {
+                const float ov[4] = {o.x, o.y, o.z, o.w};
+                for (int j = 0; j < 4; ++j)
+                  if (n + j < N) dst[j] = (EPI == QVIT_EPI_F32_RESID) ? dst[j] + ov[j] : ov[j];
+              }
+            } else {
+              const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
+              float v[4], k[4];
+              bool need[4];
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                v[j] = alpha * (float)a4[j] + bb[j];
+                if (EPI == QVIT_EPI_I8_GELU) v[j] = gelu_ref(v[j]);
+                k[j] = quant_fast(v[j], qp, need[j]);
+              }
+              if (__any(need[0] | need[1] | need[2] | need[3])) {  // rare: near-tie elements
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                  if (need[j]) k[j] = quant_fixup(v[j], qp);
+              }
+              uint32_t word = 0;
+#pragma unroll
+              for (int j = 0; j < 4; ++j) word |= ((uint32_t)(uint8_t)to_i8_sat(k[j])) << (8 * j);
+              int8_t* dst = reinterpret_cast<int8_t*>(C) + (int64_t)m * ldc + n;
+              if (nfull) {
+                *reinterpret_cast<uint32_t*>(dst) = word;
+              } else {
+                for (int j = 0; j < 4; ++j)
+                  if (n + j < N) dst[j] = (int8_t)((word >> (8 * j)) & 0xff);
+              }
             }
-            *reinterpret_cast<float4*>(dst) = o;
-          } else {
-            const float ov[4] = {o.x, o.y, o.z, o.w};
-            for (int j = 0; j < 4; ++j)
-              if (n + j < N) dst[j] = (EPI == QVIT_EPI_F32_RESID) ? dst[j] + ov[j] : ov[j];
-          }
-        } else {
-          const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
-          float v[4], k[4];
-          bool need[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            v[j] = alpha * (float)a4[j] + bb[j];
-            if (EPI == QVIT_EPI_I8_GELU) v[j] = gelu_ref(v[j]);
-            k[j] = quant_fast(v[j], qp, need[j]);
-          }
-          if (__any(need[0] | need[1] | need[2] | need[3])) {  // rare: near-tie elements
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (need[j]) k[j] = quant_fixup(v[j], qp);
-          }
-          uint32_t word = 0;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) word |= ((uint32_t)(uint8_t)to_i8_sat(k[j])) << (8 * j);
-          int8_t* dst = reinterpret_cast<int8_t*>(C) + (int64_t)m * ldc + n;
-          if (nfull) {
-            *reinterpret_cast<uint32_t*>(dst) = word;
-          } else {
-            for (int j = 0; j < 4; ++j)
-              if (n + j < N) dst[j] = (int8_t)((word >> (8 * j)) & 0xff);
           }
         }
       }
     }
-    __syncthreads();
+    }
+    if (!has_next) break;
+    t = tnext;
+    cs = ns;
+    g += nk;
   }
-  QVIT_STAMP(4);
-  QVIT_STAMP_FLUSH;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+int device_cus() {
+  static int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess || n <= 0)
+      n = 256;
+    return n;
+  }();
+  return cus;
 }
 
 template <int WFMT, int EPI>
 int launch(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int64_t N, int64_t npad,
            void* C, int64_t ldc, const EpiArgs& ep, hipStream_t stream) {
   using G = Geo<WFMT, 1>;
-  const int64_t nblk = (npad / BN) * ((M + G::BM - 1) / G::BM);
-  const int8_t* W = reinterpret_cast<const int8_t*>(Wp);
-  if (K == KTILE)
-    hipLaunchKernelGGL((gemm_kernel<WFMT, EPI, 1, true>), dim3((unsigned)nblk), dim3(G::NT), 0, stream, A, (int)M,
-                       (int)K, lda, W, (int)N, (int)npad, C, ldc, ep);
-  else
-    hipLaunchKernelGGL((gemm_kernel<WFMT, EPI, 1, false>), dim3((unsigned)nblk), dim3(G::NT), 0, stream, A, (int)M,
-                       (int)K, lda, W, (int)N, (int)npad, C, ldc, ep);
+  const int64_t ntiles = (npad / BN) * ((M + G::BM - 1) / G::BM);
+  // resident blocks, a multiple of 8 (one team per XCD), no more than the tiles need
+  int64_t grid = (int64_t)device_cus() * G::MIN_BLOCKS / 8 * 8;
+  const int64_t need = (ntiles + 7) / 8 * 8;
+  if (grid > need) grid = need;
+  if (grid < 8) grid = 8;
+  hipLaunchKernelGGL((gemm_kernel<WFMT, EPI, 1>), dim3((unsigned)grid), dim3(G::NT), 0, stream, A, (int)M, (int)K,
+                     lda, reinterpret_cast<const int8_t*>(Wp), (int)N, (int)npad, C, ldc, ep);
   return qvit_hip_status(hipGetLastError());
 }
 
