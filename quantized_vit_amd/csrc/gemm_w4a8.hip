@@ -140,7 +140,7 @@ struct EpiArgs {
 // the direct epilogue evaluates, and validated (both ends constant, no bucket whose end codes differ
 // by more than one); an invalid table makes the epilogue fall back to the direct computation.
 struct EpiTableHdr {
-  float v_lo;
+  float c0;     // -v_lo * inv_w (rounded): bucket(v) = clamp(int(fma(v, inv_w, c0)), 0, nb - 1)
   float inv_w;
   int nb;
   int valid;
@@ -150,9 +150,31 @@ struct EpiTableEnt {
   int8_t lo, hi;
   int16_t pad;
 };
-QVIT_DEV int epi_bucket(float v, float v_lo, float inv_w, int nb) {
-  const float f = __fmul_rn(__fsub_rn(v, v_lo), inv_w);
-  return (int)fminf(fmaxf(f, 0.f), (float)(nb - 1));  // NaN -> 0
+// Monotone in v (the bisection in the builder relies on it); one FMA and one med3 in the epilogue.
+QVIT_DEV int epi_bucket(float v, float c0, float inv_w, float nbm1) {
+  return (int)__builtin_amdgcn_fmed3f(fmaf(v, inv_w, c0), 0.f, nbm1);
+}
+
+// wd.byte[J] = (v >= thr) ? byte 1 of lohi : byte 0 of lohi (J = 0 also zeroes bytes 1..3):
+// a v_cmp and one SDWA v_cndmask that writes the selected byte in place.
+template <int J>
+QVIT_DEV void epi_select_byte(uint32_t& wd, float v, float thr, uint32_t lohi) {
+  if (J == 0)
+    asm("v_cmp_ge_f32_e32 vcc, %1, %2\n\t"
+        "v_cndmask_b32_sdwa %0, %3, %3, vcc dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:BYTE_1"
+        : "=v"(wd) : "v"(v), "v"(thr), "v"(lohi) : "vcc");
+  else if (J == 1)
+    asm("v_cmp_ge_f32_e32 vcc, %1, %2\n\t"
+        "v_cndmask_b32_sdwa %0, %3, %3, vcc dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_0 src1_sel:BYTE_1"
+        : "+v"(wd) : "v"(v), "v"(thr), "v"(lohi) : "vcc");
+  else if (J == 2)
+    asm("v_cmp_ge_f32_e32 vcc, %1, %2\n\t"
+        "v_cndmask_b32_sdwa %0, %3, %3, vcc dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_0 src1_sel:BYTE_1"
+        : "+v"(wd) : "v"(v), "v"(thr), "v"(lohi) : "vcc");
+  else
+    asm("v_cmp_ge_f32_e32 vcc, %1, %2\n\t"
+        "v_cndmask_b32_sdwa %0, %3, %3, vcc dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_0 src1_sel:BYTE_1"
+        : "+v"(wd) : "v"(v), "v"(thr), "v"(lohi) : "vcc");
 }
 
 QVIT_DEV float epi_F(float v, int gelu, const QParams& qp) { return quant_code(gelu ? gelu_ref(v) : v, qp); }
@@ -165,13 +187,13 @@ QVIT_DEV int fkey(float f) {
 QVIT_DEV float funkey(int k) { return __int_as_float(k >= 0 ? k : (int)(0x80000000u - (unsigned)k)); }
 
 __global__ void epi_table_kernel(int gelu, int out_qtype, const float* out_d, const float* out_qm, const float* out_t,
-                                 int out_levels, float v_lo, float inv_w, int nb, int8_t* table) {
+                                 int out_levels, float c0, float inv_w, int nb, int8_t* table) {
   const QParams qp = load_qparams(out_qtype, out_d, out_qm, out_t, out_levels);
   EpiTableHdr* hdr = reinterpret_cast<EpiTableHdr*>(table);
   EpiTableEnt* ent = reinterpret_cast<EpiTableEnt*>(table + sizeof(EpiTableHdr));
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j == 0) {
-    hdr->v_lo = v_lo;
+    hdr->c0 = c0;
     hdr->inv_w = inv_w;
     hdr->nb = nb;
   }
@@ -181,7 +203,7 @@ __global__ void epi_table_kernel(int gelu, int out_qtype, const float* out_d, co
     int lo = fkey(-3.0e38f), hi = fkey(3.0e38f);
     while (lo < hi) {
       const int mid = lo + ((hi - lo) >> 1);
-      if (epi_bucket(funkey(mid), v_lo, inv_w, nb) >= b) hi = mid;
+      if (epi_bucket(funkey(mid), c0, inv_w, (float)(nb - 1)) >= b) hi = mid;
       else lo = mid + 1;
     }
     return lo;
@@ -291,12 +313,12 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   float alpha = 0.f;
   if (EPI != QVIT_EPI_I32) alpha = (*ep.d_act) * (*ep.d_wt);
   bool use_table = false;
-  float t_vlo = 0.f, t_invw = 0.f;
+  float t_c0 = 0.f, t_invw = 0.f;
   int t_nb = 1;
   if (I8OUT && ep.table != nullptr) {
     const EpiTableHdr h = *reinterpret_cast<const EpiTableHdr*>(ep.table);
     use_table = h.valid != 0 && h.nb <= G::TABLE_MAX_NB;
-    t_vlo = h.v_lo;
+    t_c0 = h.c0;
     t_invw = h.inv_w;
     t_nb = h.nb;
     if (use_table) {  // -> the epilogue region, once per block (made visible by the first stage sync)
@@ -398,6 +420,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   issue(cs, 0, 0);
   issue(cs, 1, 1);
   Frags<WFMT> fa, fb;
+  QVIT_STAMP_DECL
   for (;;) {
     const int tnext = t + team;
     const bool has_next = tnext < hi;
@@ -411,8 +434,10 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     // head: stage 0 of this tile landed (stage 1 may still be in flight); every wave is past the
     // previous tile's epilogue, so the tile's bias can be DMA'd into its LDS slot (1 KiB, wave 0;
     // older than every later stage DMA, so the counted stage waits cover it)
+    QVIT_STAMP(5);
     __builtin_amdgcn_s_waitcnt(0xC07F);
     stage_sync<D>();
+    QVIT_STAMP(0);
     if (has_bias && wave == 0)
       dma16(ep.bias + n0 + lane_opaque() * 4, __builtin_amdgcn_readfirstlane(lds0 + G::RING_BYTES + G::EPI_BYTES));
     read_frags(g % RING, fa);
@@ -422,13 +447,19 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_sched_barrier(0);
       issue(cs, kt + 2, (g + kt + 2) % RING);
+      QVIT_STAMP(1);
       stage_sync<D>();
+      QVIT_STAMP(2);
       step_core(fa, fb, (g + kt + 1) % RING, true);
+      QVIT_STAMP(3);
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_sched_barrier(0);
       issue(cs, kt + 3, (g + kt + 3) % RING);
+      QVIT_STAMP(1);
       stage_sync<D>();
+      QVIT_STAMP(2);
       step_core(fb, fa, (g + kt + 2) % RING, true);
+      QVIT_STAMP(3);
     }
     // tail kt = nk-2, nk-1: issue the next tile's stages 0, 1
     __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -444,6 +475,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     __builtin_amdgcn_sched_barrier(0);
     if (has_next) issue(ns, 1, (g + nk + 1) % RING);
     step_core(fb, fa, 0, false);
+    QVIT_STAMP(3);
 
 #if defined(QVIT_GEMM_ABL)
     if (QVIT_GEMM_ABL == 6) {  // diagnostic: no epilogue (accumulators folded into one store per lane)
@@ -463,7 +495,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     if (I8OUT && use_table) {
       // register path: lane (fr, fq) owns the 16 consecutive columns [nbase, nbase+16) of rows
       // m0 + 16 s + fr, so each accumulator row leaves as one 16-B code store
-      const EpiTableEnt* tl = reinterpret_cast<const EpiTableEnt*>(epi_lds + sizeof(EpiTableHdr));
+      const int8_t* tlb = epi_lds + sizeof(EpiTableHdr);  // 8-B entries {thr, lo | hi << 8}
       const int nbase = n0 + 64 * wn + 16 * efq;
       float bcol[16];
 #pragma unroll
@@ -476,16 +508,26 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
 #pragma unroll
       for (int sr = 0; sr < 8; ++sr) {
         const int m = m0 + 128 * wm + 16 * sr + efr;
-        uint32_t wd[4] = {0, 0, 0, 0};
+        uint32_t wd[4];
+        const float nbm1 = (float)(t_nb - 1);
+        // the row's 16 lookups are issued together, then resolved (one LDS latency per row)
+        float v[4][4];
+        uint2 e[4][4];
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const float v = fmaf(alpha, (float)acc[r][sr][j], bcol[4 * r + j]);
-            const EpiTableEnt e = tl[epi_bucket(v, t_vlo, t_invw, t_nb)];
-            const int8_t c = v >= e.thr ? e.hi : e.lo;
-            wd[r] |= ((uint32_t)(uint8_t)c) << (8 * j);
+            v[r][j] = fmaf(alpha, (float)acc[r][sr][j], bcol[4 * r + j]);
+            e[r][j] = *reinterpret_cast<const uint2*>(tlb + (epi_bucket(v[r][j], t_c0, t_invw, nbm1) << 3));
           }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          epi_select_byte<0>(wd[r], v[r][0], __uint_as_float(e[r][0].x), e[r][0].y);
+          epi_select_byte<1>(wd[r], v[r][1], __uint_as_float(e[r][1].x), e[r][1].y);
+          epi_select_byte<2>(wd[r], v[r][2], __uint_as_float(e[r][2].x), e[r][2].y);
+          epi_select_byte<3>(wd[r], v[r][3], __uint_as_float(e[r][3].x), e[r][3].y);
+        }
         if (m < M) {
           int8_t* dst = reinterpret_cast<int8_t*>(C) + (int64_t)m * ldc + nbase;
           if (nbase + 16 <= N) {
@@ -581,11 +623,13 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
       }
     }
     }
+    QVIT_STAMP(4);
     if (!has_next) break;
     t = tnext;
     cs = ns;
     g += nk;
   }
+  QVIT_STAMP_FLUSH;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -646,8 +690,8 @@ extern "C" int qvit_epi_table_build(int epilogue, int out_qtype, const float* ou
                                 hipMemcpyHostToDevice, stream);
   if (e != hipSuccess) return qvit_hip_status(e);
   hipLaunchKernelGGL(epi_table_kernel, dim3((unsigned)((nb + 63) / 64)), dim3(64), 0, stream,
-                     epilogue == QVIT_EPI_I8_GELU ? 1 : 0, out_qtype, out_d, out_qm, out_t, out_levels, v_lo, 1.0f / w,
-                     (int)nb, reinterpret_cast<int8_t*>(table));
+                     epilogue == QVIT_EPI_I8_GELU ? 1 : 0, out_qtype, out_d, out_qm, out_t, out_levels,
+                     -(v_lo * (1.0f / w)), 1.0f / w, (int)nb, reinterpret_cast<int8_t*>(table));
   return qvit_hip_status(hipGetLastError());
 }
 

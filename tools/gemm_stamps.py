@@ -5,8 +5,9 @@ prints the per-wave phase breakdown in shader cycles.
     python tools/gemm_stamps.py --build          # here (no GPU): compile tools/_diag/libqvit_hip_stamps.so
     python tools/gemm_stamps.py [--shapes fc1_i32,fc2]   # on the GPU box
 
-Phases: prologue (first 3 stages issued, stage 0 read), DMA issue, stage wait (vmcnt + barrier),
-fragment reads + MFMA issue, epilogue, and the step-top LDS drain. Stamps cost cycles themselves;
+Phases of the persistent kernel, summed over a wave's tiles: tile head (stage-0 wait), DMA issue,
+stage wait (vmcnt + barrier), fragment reads + MFMA issue (incl. the two tail steps), epilogue, and
+tile setup (next-tile sources, accumulator reset). Stamps cost cycles themselves;
 compare phases within one run, not against the product library's wall time.
 """
 import argparse
@@ -18,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 DIAG = os.path.join(ROOT, "tools", "_diag")
 LIB = os.path.join(DIAG, "libqvit_hip_stamps.so")
-PHASES = ["prologue", "dma_issue", "stage_wait", "reads+mfma", "epilogue", "step_drain"]
+PHASES = ["head_wait", "dma_issue", "stage_wait", "reads+mfma", "epilogue", "tile_setup"]
 
 
 def main():
@@ -30,8 +31,20 @@ def main():
                     help="with --build: also build timing-only ablation libraries (1 no DMA, "
                          "4 contiguous L2-hot pieces, 5 per-row pieces on L2-hot rows)")
     ap.add_argument("--bench-abl", type=int, default=0, help="time ablation library N (no stamps)")
+    ap.add_argument("--build-var", nargs="*", default=[],
+                    help="NAME=DEF1,DEF2 ...: build tools/_diag/libqvit_hip_NAME.so with those defines")
+    ap.add_argument("--bench-var", default="", help="time variant library NAME (see --build-var)")
     a = ap.parse_args()
     from quantized_vit_amd import build
+    if a.build_var:
+        for spec in a.build_var:
+            name, defs = spec.split("=", 1)
+            print(build.build(defines=tuple(d for d in defs.split(",") if d),
+                              lib=os.path.join(DIAG, f"libqvit_hip_{name}.so"),
+                              build_dir=os.path.join(DIAG, f"obj_{name}")))
+        return
+    if a.bench_var:
+        a.bench_abl = a.bench_var
     if a.build:
         print(build.build(defines=("QVIT_GEMM_STAMPS",), lib=LIB, build_dir=os.path.join(DIAG, "obj")))
         for n in a.abl:
@@ -43,11 +56,12 @@ def main():
         from quantized_vit_amd import _lib
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         import gemm_bench
-        _lib.load(os.path.join(DIAG, f"libqvit_hip_abl{a.bench_abl}.so"))
+        tag = a.bench_abl if isinstance(a.bench_abl, str) else f"abl{a.bench_abl}"
+        _lib.load(os.path.join(DIAG, f"libqvit_hip_{tag}.so"))
         for name in a.shapes.split(","):
             M, N, K, epi = gemm_bench.SHAPES[name]
             r = gemm_bench.run(name, M, N, K, epi, 20, torch.device("cuda:0"))
-            print(f"abl{a.bench_abl} {name:8s} {r['ms']*1e3:8.1f} us  {100*r['frac']:5.1f}% of int8 peak", flush=True)
+            print(f"{tag} {name:8s} {r['ms']*1e3:8.1f} us  {100*r['frac']:5.1f}% of int8 peak", flush=True)
         return
     import torch
     from quantized_vit_amd import _lib
@@ -69,7 +83,9 @@ def main():
         per = [buf[i] / waves for i in range(6)]
         tot = sum(per)
         nk = K // 64
-        mfma_cyc = 32 * nk * 16  # 32 MFMAs of 16 cycles per stage, one wave alone on its SIMD
+        tiles = ((N + 255) // 256) * ((M + 127) // 128)
+        blocks = min(tiles + (-tiles) % 8, torch.cuda.get_device_properties(0).multi_processor_count * 2)
+        mfma_cyc = int(32 * nk * 16 * tiles / blocks)  # 32 MFMAs of 16 cycles per stage, per wave
         print(f"{name:8s} {r['ms']*1e3:7.1f} us  cycles/wave {tot:9.0f}  (MFMA floor {mfma_cyc})  " +
               "  ".join(f"{p} {v:7.0f} ({100*v/tot:4.1f}%)" for p, v in zip(PHASES, per)), flush=True)
 

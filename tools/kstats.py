@@ -17,7 +17,7 @@ import re
 import statistics
 import sys
 
-FC1_KERNEL = re.compile(r"gemm_kernel<4, 2, 1, false>")  # W4 weights, I8_GELU epilogue, K > 128
+FC1_KERNEL = re.compile(r"gemm_kernel<4, 2, 1>")  # W4 weights, I8_GELU epilogue, 4 waves
 
 
 def top(path, n=25):
