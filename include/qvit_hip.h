@@ -70,6 +70,8 @@ extern "C" {
 #define QVIT_EPI_I8_GELU    2  /* C[m,n]  = q_next(gelu(d_act d_wt acc + bias[n]))  (int8 codes)    */
 #define QVIT_EPI_I8         3  /* C[m,n]  = q_next(d_act d_wt acc + bias[n])        (int8 codes)    */
 #define QVIT_EPI_I32        4  /* C[m,n]  = acc                                      (int32, exact)  */
+#define QVIT_EPI_QKV_SPLIT  5  /* fp16 hi/lo planes of in_scale (d_act d_wt acc + bias[n]); only via
+                                  qvit_gemm_qkv_split (qvit_gemm rejects it)                        */
 
 /* ---- qvit_ultra_conv epilogues (UltraNet, 4-bit quantization/mymodel.py) -------------------- */
 #define QVIT_ULTRA_CODES       0  /* codes = rne(clamp(bn(acc/den), 0, 1) (2^a_bit-1))       (uint codes) */
@@ -243,6 +245,29 @@ int qvit_attention(const float* qkv, int64_t B, int64_t N, int64_t H, int64_t he
                    float scale, float in_scale, int out_mode, void* out, int64_t ldo,
                    int out_qtype, const float* out_d, const float* out_qm, const float* out_t,
                    int out_levels, hipStream_t stream);
+
+/*
+ * The qkv projection feeding qvit_attention_split (fused block path; replaces the fp32 qkv of
+ * Attention.forward, vit_model.py:130-137, with the operand form the attention kernel consumes).
+ * The value x = d_act d_wt acc + bias[n] is computed exactly as QVIT_EPI_F32 does, scaled by the power
+ * of two in_scale and split into fp16 hi = f16(x s), lo = f16(x s - hi), stored head-major:
+ *   qkv_hi / qkv_lo : fp16 [B][N / 64][seq][64], B = M / seq, plane p = n / 64 (q heads, k heads,
+ *                     v heads), element (b, p, t, n % 64) for row m = b seq + t; 16-B aligned.
+ * A, Wp, d_act, d_wt, bias as qvit_gemm; N % 64 == 0, M % seq == 0.
+ */
+int qvit_gemm_qkv_split(const int8_t* A, int64_t M, int64_t K, int64_t lda,
+                        const void* Wp, int wfmt, int64_t N, int64_t npad,
+                        const float* d_act, const float* d_wt, const float* bias,
+                        int64_t seq, float in_scale, void* qkv_hi, void* qkv_lo, hipStream_t stream);
+
+/*
+ * qvit_attention on the split operands of qvit_gemm_qkv_split (planes [B][3H][N][64], in_scale the
+ * same power of two): identical arithmetic; K/V blocks stream into LDS by DMA with no conversion.
+ */
+int qvit_attention_split(const void* qkv_hi, const void* qkv_lo, int64_t B, int64_t N, int64_t H,
+                         int64_t head_dim, float scale, float in_scale, int out_mode, void* out,
+                         int64_t ldo, int out_qtype, const float* out_d, const float* out_qm,
+                         const float* out_t, int out_levels, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -30,6 +30,7 @@ EPI_F32_RESID = 1
 EPI_I8_GELU = 2
 EPI_I8 = 3
 EPI_I32 = 4
+EPI_QKV_SPLIT = 5   # qvit_gemm_qkv_split only
 
 ATT_F32 = 0
 ATT_I8 = 1
@@ -69,6 +70,10 @@ _SIGNATURES = {
     "qvit_yolo_decode": [_c_p, _i64, _i64, _i64, _i64, _i64, _i64, _c_p, _f32, _c_p, _c_p, _c_p],
     "qvit_attention": [_c_p, _i64, _i64, _i64, _i64, _i64, _f32, _f32, _i32, _c_p, _i64, _i32, _c_p, _c_p, _c_p,
                        _i32, _c_p],
+    "qvit_gemm_qkv_split": [_c_p, _i64, _i64, _i64, _c_p, _i32, _i64, _i64, _c_p, _c_p, _c_p, _i64, _f32, _c_p,
+                            _c_p, _c_p],
+    "qvit_attention_split": [_c_p, _c_p, _i64, _i64, _i64, _i64, _f32, _f32, _i32, _c_p, _i64, _i32, _c_p, _c_p,
+                             _c_p, _i32, _c_p],
 }
 STRING_FUNCS = {"qvit_strerror": [_i32], "qvit_version": []}
 EXPORTED_SYMBOLS = sorted(list(_SIGNATURES) + list(STRING_FUNCS))
@@ -220,6 +225,32 @@ def attention(qkv: torch.Tensor, B: int, N: int, H: int, head_dim: int, scale: f
     _check(load().qvit_attention(_ptr(qkv), B, N, H, head_dim, qkv.stride(0), scale, in_scale, out_mode, _ptr(out),
                                  out.stride(0), out_qtype, _ptr(out_d), _ptr(out_qm), _ptr(out_t), out_levels,
                                  _stream(qkv.device)), "qvit_attention")
+    return out
+
+
+def gemm_qkv_split(A: torch.Tensor, M: int, K: int, packed: torch.Tensor, wfmt: int, N: int, npad: int,
+                   d_act: torch.Tensor, d_wt: torch.Tensor, bias_pad: Optional[torch.Tensor], seq: int,
+                   in_scale: float, hi: torch.Tensor, lo: torch.Tensor):
+    """qkv projection as fp16 hi/lo planes [B][N/64][seq][64] of in_scale * x (qvit_gemm_qkv_split)."""
+    _require_gpu(A, "codes")
+    assert hi.dtype == torch.float16 and lo.dtype == torch.float16 and hi.is_contiguous() and lo.is_contiguous()
+    assert hi.numel() >= M * N and lo.numel() >= M * N
+    _check(load().qvit_gemm_qkv_split(_ptr(A), M, K, A.stride(0), _ptr(packed), wfmt, N, npad, _ptr(d_act),
+                                      _ptr(d_wt), _ptr(bias_pad), seq, in_scale, _ptr(hi), _ptr(lo),
+                                      _stream(A.device)), "qvit_gemm_qkv_split")
+    return hi, lo
+
+
+def attention_split(hi: torch.Tensor, lo: torch.Tensor, B: int, N: int, H: int, head_dim: int, scale: float,
+                    out: torch.Tensor, out_mode: int = ATT_F32, in_scale: float = 1.0, out_qtype: int = 0,
+                    out_d=None, out_qm=None, out_t=None, out_levels: int = 0) -> torch.Tensor:
+    """qvit_attention on the split planes of gemm_qkv_split."""
+    _require_gpu(hi, "qkv_hi")
+    assert hi.dtype == torch.float16 and lo.dtype == torch.float16
+    assert hi.numel() >= B * 3 * H * N * head_dim and lo.numel() >= B * 3 * H * N * head_dim
+    _check(load().qvit_attention_split(_ptr(hi), _ptr(lo), B, N, H, head_dim, scale, in_scale, out_mode, _ptr(out),
+                                       out.stride(0), out_qtype, _ptr(out_d), _ptr(out_qm), _ptr(out_t), out_levels,
+                                       _stream(hi.device)), "qvit_attention_split")
     return out
 
 

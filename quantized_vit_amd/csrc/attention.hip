@@ -24,6 +24,8 @@
 //   V: 32-B block b of row r at b ^ ((r >> 1) & 3)        (ds_read_b64_tr_b16 transposed reads)
 #include "qvit_common.h"
 
+#include <algorithm>
+
 namespace {
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
@@ -72,15 +74,167 @@ QVIT_DEV f4 mfma3(h8 ah, h8 al, h8 bh, h8 bl, f4 c) {
   return c;
 }
 
+// Cross-lane max / sum over the 4 lane groups g (xor 16, xor 32) with the gfx950 permlane swaps (VALU,
+// no LDS round trip); the sums add in the same order as a butterfly of shuffles.
 QVIT_DEV float xmax(float v) {
-  v = fmaxf(v, __shfl_xor(v, 16));
-  return fmaxf(v, __shfl_xor(v, 32));
+#if defined(QVIT_ATT_ABL) && QVIT_ATT_ABL == 3
+  return v;  // diagnostic: no cross-lane step
+#endif
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
 }
 QVIT_DEV float xsum(float v) {
-  v += __shfl_xor(v, 16);
-  return v + __shfl_xor(v, 32);
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
+// Online-softmax update of one key block (KB keys in the LDS images at st) for a wave's first NT query
+// tiles, in three phases that keep the live fragments small (2 waves per SIMD leave 256 registers):
+//   1. S^T = K . Q^T for every tile (K fragments live only here);
+//   2. the softmax of every tile: running max / sum, P split to fp16 hi/lo in place of the scores;
+//   3. O^T += V^T . P^T one 16-dim slice at a time (one V fragment pair live).
+// No branches between the tiles: the softmax of tile i runs while the matrix core finishes the later
+// tiles' scores, and the first slices' PV products overlap the last softmaxes.
+// s[i][kt][j] = S^T[key kbase + 16 kt + j][query of the lane]; scores in log2 units (sl2).
+// MASK: the block holds keys >= N (the last block only).
+QVIT_DEV void attend(int nt, bool mask, const int8_t* st, const h8 (&qh)[QTW][2], const h8 (&ql)[QTW][2], float (&m)[QTW],
+                     float (&l)[QTW], f4 (&o)[QTW][4], const int (&koffs)[2][2], const int (&voffs)[4], int kbase,
+                     int N, float sl2) {
+#if defined(QVIT_ATT_ABL) && QVIT_ATT_ABL == 1
+  return;  // diagnostic: operand streaming only
+#endif
+  constexpr int NT = QTW;
+  f4 s[NT][2];
+  {
+    h8 kh[2][2], kl[2][2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        kh[kt][c] = lds_h8(st, koffs[kt][c]);
+        kl[kt][c] = lds_h8(st + IMG, koffs[kt][c]);
+      }
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        s[i][kt] = f4{0.f, 0.f, 0.f, 0.f};
+        if (i == NT - 1 && nt < NT) continue;  // wave-uniform: no 4th tile
+#pragma unroll
+        for (int c = 0; c < 2; ++c) s[i][kt] = mfma3(kh[kt][c], kl[kt][c], qh[i][c], ql[i][c], s[i][kt]);
+      }
+  }
+  h8 ph[NT], pl[NT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    if (i == NT - 1 && nt < NT) continue;
+    float x[8];
+#if defined(QVIT_ATT_ABL) && QVIT_ATT_ABL == 2
+    {  // diagnostic: MFMAs only (P = raw scores)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = s[i][e >> 2][e & 3];
+      split8(x, ph[i], pl[i]);
+      continue;
+    }
+#endif
+    float bm = -INFINITY;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      x[e] = s[i][e >> 2][e & 3] * sl2;
+    }
+    if (mask) {  // wave-uniform: the last key block only
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = (kbase + 16 * (e >> 2) + (e & 3) < N) ? x[e] : -INFINITY;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bm = fmaxf(bm, x[e]);
+    bm = xmax(bm);
+    const float mn = fmaxf(m[i], bm);
+    const float alpha = __builtin_amdgcn_exp2f(m[i] - mn);
+    float ps = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      x[e] = __builtin_amdgcn_exp2f(x[e] - mn);
+      ps += x[e];
+    }
+    l[i] = l[i] * alpha + ps;
+    m[i] = mn;
+    split8(x, ph[i], pl[i]);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[i][dt] = o[i][dt] * alpha;
+  }
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    const h8 vh = join(tr_read(st + 2 * IMG, voffs[dt]), tr_read(st + 2 * IMG, voffs[dt] + 16 * 128));
+    const h8 vl = join(tr_read(st + 3 * IMG, voffs[dt]), tr_read(st + 3 * IMG, voffs[dt] + 16 * 128));
+#pragma unroll
+    for (int i = 0; i < NT - 1; ++i) o[i][dt] = mfma3(vh, vl, ph[i], pl[i], o[i][dt]);
+    if (nt == NT) o[NT - 1][dt] = mfma3(vh, vl, ph[NT - 1], pl[NT - 1], o[NT - 1][dt]);
+  }
+}
+
+// nt >= 3 (the fused shapes) or the general case: tiles past nt are skipped (wave-uniform branches).
+QVIT_DEV void attend_n(int nt, bool mask, const int8_t* st, const h8 (&qh)[QTW][2], const h8 (&ql)[QTW][2],
+                       float (&m)[QTW], float (&l)[QTW], f4 (&o)[QTW][4], const int (&koffs)[2][2],
+                       const int (&voffs)[4], int kbase, int N, float sl2) {
+  attend(nt, mask, st, qh, ql, m, l, o, koffs, voffs, kbase, N, sl2);
+}
+
+// Normalise and write a wave's query tiles: fp32 rows, or the next layer's int8 codes.
+template <int OUT>
+QVIT_DEV void attend_store(const bool (&tv)[QTW], const float (&l)[QTW], const f4 (&o)[QTW][4], int qtile0, int q0,
+                           int N, int b, int h, float in_scale, void* out, int64_t ldo, const QParams& qp) {
+  const int lane = threadIdx.x & 63;
+  const int fr = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < QTW; ++i) {
+    if (!tv[i]) continue;
+    const float inv = 1.f / (xsum(l[i]) * in_scale);
+    const int q = q0 + 16 * (qtile0 + NWAVES * i) + fr;
+    if (q >= N) continue;
+    const int64_t row = (int64_t)b * N + q;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int col = h * HD + 16 * dt + 4 * g;
+      f4 v = o[i][dt] * inv;
+      if (OUT == 0) {
+        *reinterpret_cast<f4*>(reinterpret_cast<float*>(out) + row * ldo + col) = v;
+      } else {
+        float k[4];
+        bool need[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) k[j] = quant_fast(v[j], qp, need[j]);
+        if (need[0] | need[1] | need[2] | need[3]) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (need[j]) k[j] = quant_fixup(v[j], qp);
+        }
+        uint32_t word = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) word |= ((uint32_t)(uint8_t)to_i8_sat(k[j])) << (8 * j);
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<int8_t*>(out) + row * ldo + col) = word;
+      }
+    }
+  }
+}
+
+QVIT_DEV void fragment_offsets(int (&koffs)[2][2], int (&voffs)[4]) {
+  const int lane = threadIdx.x & 63;
+  const int fr = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) koffs[kt][c] = koff(16 * kt + fr, g + 4 * c);
+  const int vq = fr >> 2, vp = fr & 3;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) voffs[dt] = voff(4 * g + vq, 2 * (16 * dt + 4 * vp));
+}
+
+// ---- fp32 qkv input (the unfused module path) -------------------------------------------------------
 template <int OUT>  // 0: fp32 output, 1: int8 codes of the next layer's activation quantizer
 __global__ __launch_bounds__(256, 2) void attn_kernel(const float* __restrict__ qkv, int N, int H, int64_t ldq,
                                                       float scale, float in_scale, void* __restrict__ out,
@@ -90,7 +244,7 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const float* __restrict__ 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int fr = lane & 15;  // query (S^T column) / key row of an A fragment / dim row of V^T
+  const int fr = lane & 15;
   const int g = lane >> 4;
 
   const int ngroups = (N + QG - 1) / QG;
@@ -156,16 +310,8 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const float* __restrict__ 
     *reinterpret_cast<h8*>(st + 3 * IMG + voff(srow, 16 * schunk)) = lo;
   };
 
-  // per-lane fragment offsets
-  int koffs[2][2];
-#pragma unroll
-  for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-    for (int c = 0; c < 2; ++c) koffs[kt][c] = koff(16 * kt + fr, g + 4 * c);
-  const int vq = fr >> 2, vp = fr & 3;
-  int voffs[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) voffs[dt] = voff(4 * g + vq, 2 * (16 * dt + 4 * vp));
+  int koffs[2][2], voffs[4];
+  fragment_offsets(koffs, voffs);
 
   // softmax state and O^T accumulators: o[i][dt][j] = O^T[16 dt + 4 g + j][query of lane]
   const float sl2 = scale * LOG2E / (in_scale * in_scale);
@@ -179,104 +325,193 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const float* __restrict__ 
     for (int dt = 0; dt < 4; ++dt) o[i][dt] = f4{0.f, 0.f, 0.f, 0.f};
   }
 
+  int nt = 0;  // valid tiles of this wave (a prefix of i = 0..3)
+#pragma unroll
+  for (int i = 0; i < QTW; ++i) nt += tv[i] ? 1 : 0;
   const int nkb = (N + KB - 1) / KB;
   load_block(0);
   store_block(0);
   __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
     if (kb + 1 < nkb) load_block(kb + 1);
-    const int8_t* st = smem + (kb & 1) * STAGE;
-    h8 kh[2][2], kl[2][2], vh[4], vl[4];
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        kh[kt][c] = lds_h8(st, koffs[kt][c]);
-        kl[kt][c] = lds_h8(st + IMG, koffs[kt][c]);
-      }
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      vh[dt] = join(tr_read(st + 2 * IMG, voffs[dt]), tr_read(st + 2 * IMG, voffs[dt] + 16 * 128));
-      vl[dt] = join(tr_read(st + 3 * IMG, voffs[dt]), tr_read(st + 3 * IMG, voffs[dt] + 16 * 128));
-    }
-    const int kbase = kb * KB + 4 * g;
-#pragma unroll
-    for (int i = 0; i < QTW; ++i) {
-      if (!tv[i]) continue;  // wave-uniform
-      f4 s[2];
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        s[kt] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int c = 0; c < 2; ++c) s[kt] = mfma3(kh[kt][c], kl[kt][c], qh[i][c], ql[i][c], s[kt]);
-      }
-      // s[kt][j] = S^T[key kbase + 16 kt + j][query]; scores in log2 units
-      float x[8];
-      float bm = -INFINITY;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float v = (kbase + 16 * kt + j < N) ? s[kt][j] * sl2 : -INFINITY;
-          x[4 * kt + j] = v;
-          bm = fmaxf(bm, v);
-        }
-      bm = xmax(bm);
-      const float mn = fmaxf(m[i], bm);
-      const float alpha = __builtin_amdgcn_exp2f(m[i] - mn);
-      float ps = 0.f;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        x[e] = __builtin_amdgcn_exp2f(x[e] - mn);
-        ps += x[e];
-      }
-      l[i] = l[i] * alpha + ps;
-      m[i] = mn;
-      h8 ph, pl;
-      split8(x, ph, pl);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) o[i][dt] = mfma3(vh[dt], vl[dt], ph, pl, o[i][dt] * alpha);
-    }
+    attend_n(nt, (kb + 1) * KB > N, smem + (kb & 1) * STAGE, qh, ql, m, l, o, koffs, voffs, kb * KB + 4 * g, N,
+             sl2);
     if (kb + 1 < nkb) {
       __syncthreads();  // every wave is done with buffer (kb + 1) & 1 (used by block kb - 1)
       store_block((kb + 1) & 1);
     }
     __syncthreads();
   }
-
-  // ---- epilogue: normalise, write fp32 or the next layer's int8 codes ----------------------------
-  QParams qp;
+  QParams qp{};
   if (OUT == 1) qp = load_qparams(out_qtype, out_d, out_qm, out_t, out_levels);
+  attend_store<OUT>(tv, l, o, wave, q0, N, b, h, in_scale, out, ldo, qp);
+}
+
+// ---- split fp16 input (the fused block path) --------------------------------------------------------
+// q, k, v arrive pre-scaled and pre-split by the qkv GEMM (qvit_gemm_qkv_split): hi and lo planes of
+// layout [B][3H][N][64] fp16, so a key block's four LDS images (K hi/lo, V hi/lo; 32 rows x 128 B) are
+// copied by LDS-DMA straight from global memory, the swizzle applied on the source side. A ring of
+// SRING blocks keeps SRING - 1 blocks (48 KiB per workgroup) in flight: a head's keys stream while the
+// previous block is computed, with no register staging and no conversion in this kernel.
+constexpr int SRING = 4;
+
+QVIT_DEV uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// 64 lanes x 16 B from per-lane global addresses to lds_base + 16 * lane (M0 saved and restored).
+QVIT_DEV void dma16(const void* gsrc, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_base)
+      : "memory");
+}
+
+template <int N_>
+QVIT_DEV void block_sync() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N_) : "memory");
+}
+
+// Persistent: workgroup w walks the units (image, head, group of <= QG queries) w, w + grid, ... Each
+// unit is a run of ring blocks in one stream: nqb query blocks (64 queries: hi and lo images in the K
+// layout, wave w reads its tile from each) and then nkb key blocks. Block p + 3 is issued as soon as
+// block p is waited for, across unit boundaries, so the next unit's queries and first keys land while the
+// current unit finishes. Every global load of the loop is an LDS-DMA (the quantizer scalars are read
+// before the stream starts), so the only vmcnt waits are the counted stage waits; the output stores of a
+// unit's epilogue do join the count and are drained by the next wait.
+constexpr int QB = 64;  // queries per query block
+
+template <int OUT>
+__global__ __launch_bounds__(256, 2) void attn_split_kernel(const _Float16* __restrict__ hi,
+                                                            const _Float16* __restrict__ lo, int N, int H, int nunits,
+                                                            float scale, float in_scale, void* __restrict__ out,
+                                                            int64_t ldo, int out_qtype, const float* out_d,
+                                                            const float* out_qm, const float* out_t, int out_levels) {
+  __shared__ __attribute__((aligned(16))) int8_t smem[SRING * STAGE];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15;
+  const int g = lane >> 4;
+
+  QParams qp{};
+  if (OUT == 1) qp = load_qparams(out_qtype, out_d, out_qm, out_t, out_levels);
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): nothing of the compiler's own is pending below
+
+  const int ngroups = (N + QG - 1) / QG;
+  const int nqb = (N < QG ? (N + QB - 1) / QB : QG / QB);
+  const int nkb = (N + KB - 1) / KB;
+  const int per = nqb + nkb;
+  const int grid = gridDim.x;
+  const int my_units = (nunits - (int)blockIdx.x + grid - 1) / grid;
+  const int total = my_units * per;
+  const int64_t plane = (int64_t)N * HD;
+
+  const uint32_t lds0 = lds_addr(smem);
+  // DMA of stream block p into ring slot p % SRING
+  auto issue = [&](int p) {
+    const int j = p / per, idx = p - j * per;
+    const int unit = (int)blockIdx.x + j * grid;
+    const int grp = unit % ngroups, bh = unit / ngroups;
+    const int h = bh % H, b = bh / H;
+    const int64_t qoff = ((int64_t)b * 3 * H + h) * plane;
+    const uint32_t base = __builtin_amdgcn_readfirstlane(lds0 + (p & (SRING - 1)) * STAGE);
+    if (idx < nqb) {  // query block: rows 16w .. 16w+15 of the hi and lo images (K layout)
 #pragma unroll
-  for (int i = 0; i < QTW; ++i) {
-    if (!tv[i]) continue;
-    const float inv = 1.f / (xsum(l[i]) * in_scale);
-    const int q = q0 + 16 * (wave + NWAVES * i) + fr;
-    if (q >= N) continue;
-    const int64_t row = (int64_t)b * N + q;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const int col = h * HD + 16 * dt + 4 * g;
-      f4 v = o[i][dt] * inv;
-      if (OUT == 0) {
-        *reinterpret_cast<f4*>(reinterpret_cast<float*>(out) + row * ldo + col) = v;
-      } else {
-        float k[4];
-        bool need[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) k[j] = quant_fast(v[j], qp, need[j]);
-        if (need[0] | need[1] | need[2] | need[3]) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (need[j]) k[j] = quant_fixup(v[j], qp);
-        }
-        uint32_t word = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) word |= ((uint32_t)(uint8_t)to_i8_sat(k[j])) << (8 * j);
-        *reinterpret_cast<uint32_t*>(reinterpret_cast<int8_t*>(out) + row * ldo + col) = word;
+      for (int pc = 0; pc < 2; ++pc) {
+        const int r = 16 * wave + 8 * pc + (lane >> 3);
+        int q = grp * QG + idx * QB + r;
+        q = q < N ? q : N - 1;
+        const int kc = ((lane & 7) ^ ((r >> 1) & 7)) << 4;
+        const int64_t e = qoff + (int64_t)q * HD;
+        const uint32_t d = base + (16 * wave + 8 * pc) * 128;
+        dma16(reinterpret_cast<const int8_t*>(hi + e) + kc, __builtin_amdgcn_readfirstlane(d));
+        dma16(reinterpret_cast<const int8_t*>(lo + e) + kc, __builtin_amdgcn_readfirstlane(d + QB * 128));
       }
+    } else {          // key block: rows 8w .. 8w+7 of K hi, K lo, V hi, V lo
+      const int kb = idx - nqb;
+      const int r = 8 * wave + (lane >> 3);
+      const int sc = lane & 7;
+      int key = kb * KB + r;
+      key = key < N ? key : N - 1;  // keys past N: a valid row, masked out of the softmax
+      const int kc = (sc ^ ((r >> 1) & 7)) << 4;
+      const int vb = (((sc >> 1) ^ ((r >> 1) & 3)) << 5) | ((sc & 1) << 4);
+      const int64_t ke = qoff + H * plane + (int64_t)key * HD;
+      const int64_t ve = ke + H * plane;
+      const uint32_t d = base + wave * 1024;
+      dma16(reinterpret_cast<const int8_t*>(hi + ke) + kc, __builtin_amdgcn_readfirstlane(d));
+      dma16(reinterpret_cast<const int8_t*>(lo + ke) + kc, __builtin_amdgcn_readfirstlane(d + IMG));
+      dma16(reinterpret_cast<const int8_t*>(hi + ve) + vb, __builtin_amdgcn_readfirstlane(d + 2 * IMG));
+      dma16(reinterpret_cast<const int8_t*>(lo + ve) + vb, __builtin_amdgcn_readfirstlane(d + 3 * IMG));
     }
+  };
+  // block p landed for every wave (4 DMAs per wave per block; up to two younger blocks in flight) and
+  // every wave is done with block p - 1, whose slot block p + 3 takes
+  auto sync = [&](int p) {
+    const int ahead = total - 1 - p;
+    if (ahead >= 2) block_sync<8>();
+    else if (ahead == 1) block_sync<4>();
+    else block_sync<0>();
+    if (p + 3 < total) issue(p + 3);
+  };
+
+  int koffs[2][2], voffs[4];
+  fragment_offsets(koffs, voffs);
+  const float sl2 = scale * LOG2E / (in_scale * in_scale);
+
+  for (int p = 0; p < 3 && p < total; ++p) issue(p);
+  int p = 0;
+  for (int j = 0; j < my_units; ++j) {
+    const int unit = (int)blockIdx.x + j * grid;
+    const int grp = unit % ngroups, bh = unit / ngroups;
+    const int h = bh % H, b = bh / H;
+    const int q0 = grp * QG;
+    const int wr = (wave + unit) & (NWAVES - 1);  // the wave owning a 4th tile rotates by unit
+    h8 qh[QTW][2], ql[QTW][2];
+    int nt = 0;
+#pragma unroll
+    for (int i = 0; i < QTW; ++i) {
+      if (i < nqb) {
+        sync(p);
+        const int8_t* st = smem + (p & (SRING - 1)) * STAGE;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int off = koff(16 * wr + fr, g + 4 * c);
+          qh[i][c] = lds_h8(st, off);
+          ql[i][c] = lds_h8(st + QB * 128, off);
+        }
+        ++p;
+      } else {  // no such query block: zeros (the tile is skipped or discarded)
+        qh[i][0] = qh[i][1] = ql[i][0] = ql[i][1] = h8{};
+      }
+      nt += (i < nqb && q0 + 16 * (wr + NWAVES * i) < N) ? 1 : 0;
+    }
+    float m[QTW], l[QTW];
+    f4 o[QTW][4];
+#pragma unroll
+    for (int i = 0; i < QTW; ++i) {
+      m[i] = -INFINITY;
+      l[i] = 0.f;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[i][dt] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+    for (int kb = 0; kb < nkb; ++kb, ++p) {
+      sync(p);
+      attend_n(nt, (kb + 1) * KB > N, smem + (p & (SRING - 1)) * STAGE, qh, ql, m, l, o, koffs, voffs,
+               kb * KB + 4 * g, N, sl2);
+    }
+    bool tv[QTW];
+#pragma unroll
+    for (int i = 0; i < QTW; ++i) tv[i] = i < nt;
+    attend_store<OUT>(tv, l, o, wr, q0, N, b, h, in_scale, out, ldo, qp);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 }  // namespace
@@ -310,5 +545,47 @@ extern "C" int qvit_attention(const float* qkv, int64_t B, int64_t N, int64_t H,
   else
     hipLaunchKernelGGL(attn_kernel<1>, dim3((unsigned)nblk), dim3(256), 0, stream, qkv, (int)N, (int)H, ldq, scale,
                        in_scale, out, ldo, out_qtype, out_d, out_qm, out_t, out_levels);
+  return qvit_hip_status(hipGetLastError());
+}
+
+extern "C" int qvit_attention_split(const void* qkv_hi, const void* qkv_lo, int64_t B, int64_t N, int64_t H,
+                                    int64_t head_dim, float scale, float in_scale, int out_mode, void* out,
+                                    int64_t ldo, int out_qtype, const float* out_d, const float* out_qm,
+                                    const float* out_t, int out_levels, hipStream_t stream) {
+  if (!qkv_hi || !qkv_lo || !out) return QVIT_ENULL;
+  if (head_dim != HD) return QVIT_EINVAL;
+  if (B < 0 || N <= 0 || H <= 0 || ldo < H * HD) return QVIT_EINVAL;
+  if (B * N > INT32_MAX || N > (1 << 20) || !(in_scale > 0.f)) return QVIT_EINVAL;
+  if ((((uintptr_t)qkv_hi) & 15) || (((uintptr_t)qkv_lo) & 15)) return QVIT_EALIGN;
+  if (out_mode == QVIT_ATT_F32) {
+    if ((ldo % 4) || (((uintptr_t)out) & 15)) return QVIT_EALIGN;
+  } else if (out_mode == QVIT_ATT_I8) {
+    if ((ldo % 4) || (((uintptr_t)out) & 3)) return QVIT_EALIGN;
+    const int q = out_qtype & 0xff;
+    if (q != QVIT_QT_LINEAR && q != QVIT_QT_NONLINEAR && q != QVIT_QT_ULTRA_ACT) return QVIT_EINVAL;
+    if (q == QVIT_QT_ULTRA_ACT ? (out_levels < 1 || out_levels > 127) : (!out_d || !out_qm)) return QVIT_EINVAL;
+  } else {
+    return QVIT_EINVAL;
+  }
+  if (B == 0) return QVIT_OK;
+  const int64_t ngroups = (N + QG - 1) / QG;
+  const int64_t nblk = B * H * ngroups;
+  if (nblk > INT32_MAX) return QVIT_EINVAL;
+  const _Float16* hi = reinterpret_cast<const _Float16*>(qkv_hi);
+  const _Float16* lo = reinterpret_cast<const _Float16*>(qkv_lo);
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess || n <= 0)
+      n = 256;
+    return n;
+  }();
+  const int64_t grid = std::min<int64_t>(nblk, 2 * (int64_t)cus);  // two resident workgroups per CU
+  if (out_mode == QVIT_ATT_F32)
+    hipLaunchKernelGGL(attn_split_kernel<0>, dim3((unsigned)grid), dim3(256), 0, stream, hi, lo, (int)N, (int)H,
+                       (int)nblk, scale, in_scale, out, ldo, out_qtype, out_d, out_qm, out_t, out_levels);
+  else
+    hipLaunchKernelGGL(attn_split_kernel<1>, dim3((unsigned)grid), dim3(256), 0, stream, hi, lo, (int)N, (int)H,
+                       (int)nblk, scale, in_scale, out, ldo, out_qtype, out_d, out_qm, out_t, out_levels);
   return qvit_hip_status(hipGetLastError());
 }

@@ -127,6 +127,10 @@ struct EpiArgs {
   const float* out_t;
   int out_levels;
   const int8_t* table;  // optional code table for the I8 epilogues (qvit_epi_table_build)
+  int seq;              // QKV_SPLIT: rows per image
+  float inv_seq;        // 1 / seq (row -> image with an exact correction)
+  float in_scale;       // QKV_SPLIT: power-of-two operand scale
+  _Float16* lo;         // QKV_SPLIT: lo plane (C is the hi plane)
 };
 
 // ---- code table of the int8 epilogues --------------------------------------------------------------
@@ -543,6 +547,102 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
           }
         }
       }
+    } else if (EPI == QVIT_EPI_F32_RESID) {
+      // C += alpha acc + bias: 16 rows per pass through the wave's staging area, 16 lanes per 64-column
+      // row segment; the residual rows of pass sr + 1 are loaded while pass sr is staged and stored, so
+      // the read-modify-write pays one memory latency per tile instead of one per row
+      int* stg = reinterpret_cast<int*>(epi_lds + wave * EPI_WAVE_BYTES);
+      const int prow = el >> 4, pcol = 4 * (el & 15);
+      const int n = n0 + 64 * wn + pcol;
+      const bool nfull = n + 4 <= N;
+      float4 b4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (has_bias) b4 = *reinterpret_cast<const float4*>(bias_l + (n - n0));
+      float* Cf = reinterpret_cast<float*>(C);
+      float4 old[2][4];
+      auto load_old = [&](int sr, float4 (&ov)[4]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = m0 + 128 * wm + 16 * sr + 4 * i + prow;
+          ov[i] = (m < M && nfull) ? *reinterpret_cast<const float4*>(Cf + (int64_t)m * ldc + n)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      };
+      load_old(0, old[0]);
+#pragma unroll
+      for (int sr = 0; sr < 8; ++sr) {
+        if (sr + 1 < 8) load_old(sr + 1, old[(sr + 1) & 1]);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          *reinterpret_cast<v4i*>(stg + efr * EPI_LD + 16 * efq + 4 * r) = acc[r][sr];
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = 4 * i + prow;
+          const int m = m0 + 128 * wm + 16 * sr + row;
+          const v4i a4 = *reinterpret_cast<const v4i*>(stg + row * EPI_LD + pcol);
+          if (m < M) {
+            float4 o = make_float4(alpha * (float)a4[0] + b4.x, alpha * (float)a4[1] + b4.y,
+                                   alpha * (float)a4[2] + b4.z, alpha * (float)a4[3] + b4.w);
+            float* dst = Cf + (int64_t)m * ldc + n;
+            if (nfull) {
+              const float4 ov = old[sr & 1][i];
+              o.x += ov.x; o.y += ov.y; o.z += ov.z; o.w += ov.w;
+              *reinterpret_cast<float4*>(dst) = o;
+            } else {
+              const float v[4] = {o.x, o.y, o.z, o.w};
+              for (int j = 0; j < 4; ++j)
+                if (n + j < N) dst[j] = dst[j] + v[j];
+            }
+          }
+        }
+      }
+    } else if (EPI == QVIT_EPI_QKV_SPLIT) {
+      // fp16 hi/lo planes: 8 lanes per 64-column head-plane row, 8 columns (16 B of hi, 16 B of lo) each
+      int* stg = reinterpret_cast<int*>(epi_lds + wave * EPI_WAVE_BYTES);
+      const int prow = el >> 3, pcol = 8 * (el & 7);
+      const int nw = n0 + 64 * wn;  // the wave's head plane (N % 64 == 0: all valid or none)
+      float bb[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bb[j] = has_bias ? bias_l[nw - n0 + pcol + j] : 0.f;
+      const int64_t pstride = (int64_t)ep.seq * 64;
+#pragma unroll
+      for (int sr = 0; sr < 8; ++sr) {
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          *reinterpret_cast<v4i*>(stg + efr * EPI_LD + 16 * efq + 4 * r) = acc[r][sr];
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int row = 8 * i + prow;
+          const int m = m0 + 128 * wm + 16 * sr + row;
+          const v4i a0 = *reinterpret_cast<const v4i*>(stg + row * EPI_LD + pcol);
+          const v4i a1 = *reinterpret_cast<const v4i*>(stg + row * EPI_LD + pcol + 4);
+          if (m < M && nw < N) {
+            int bimg = (int)((float)m * ep.inv_seq);
+            bimg -= (bimg * ep.seq > m) ? 1 : 0;
+            bimg += ((bimg + 1) * ep.seq <= m) ? 1 : 0;
+            const int tok = m - bimg * ep.seq;
+            const int64_t e = ((int64_t)bimg * (N >> 6) + (nw >> 6)) * pstride + (int64_t)tok * 64 + pcol;
+            uint32_t hw[4], lw[4];
+#pragma unroll
+            for (int j = 0; j < 8; j += 2) {
+              const int a_0 = (j < 4) ? a0[j] : a1[j - 4], a_1 = (j < 4) ? a0[j + 1] : a1[j - 3];
+              const float x0 = (alpha * (float)a_0 + bb[j]) * ep.in_scale;
+              const float x1 = (alpha * (float)a_1 + bb[j + 1]) * ep.in_scale;
+              const _Float16 h0 = (_Float16)x0, h1 = (_Float16)x1;
+              const _Float16 l0 = (_Float16)(x0 - (float)h0), l1 = (_Float16)(x1 - (float)h1);
+              hw[j >> 1] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+              lw[j >> 1] = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+            }
+            *reinterpret_cast<uint4*>(reinterpret_cast<_Float16*>(C) + e) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+            *reinterpret_cast<uint4*>(ep.lo + e) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+          }
+        }
+      }
     } else {
       // staged path: 16 accumulator rows at a time through this wave's own staging area, then 16 lanes
       // own one contiguous 64-column row segment (256-B fp32 rows / 64-B code rows); wave-local only
@@ -668,6 +768,8 @@ int dispatch_epi(int epilogue, const int8_t* A, int64_t M, int64_t K, int64_t ld
     case QVIT_EPI_I8_GELU: return launch<WFMT, QVIT_EPI_I8_GELU>(A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
     case QVIT_EPI_I8: return launch<WFMT, QVIT_EPI_I8>(A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
     case QVIT_EPI_I32: return launch<WFMT, QVIT_EPI_I32>(A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
+    case QVIT_EPI_QKV_SPLIT:
+      return launch<WFMT, QVIT_EPI_QKV_SPLIT>(A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
     default: return QVIT_EINVAL;
   }
 }
@@ -720,7 +822,7 @@ extern "C" int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda, con
   if (M == 0) return QVIT_OK;
   if (epi_table && (((uintptr_t)epi_table) & 15)) return QVIT_EALIGN;
   EpiArgs ep{d_act, d_wt, bias, out_qtype, out_d, out_qm, out_t, out_levels,
-             (i8out ? reinterpret_cast<const int8_t*>(epi_table) : nullptr)};
+             (i8out ? reinterpret_cast<const int8_t*>(epi_table) : nullptr), 1, 1.f, 1.f, nullptr};
   if (wfmt == QVIT_W4) return dispatch_epi<QVIT_W4>(epilogue, A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
   return dispatch_epi<QVIT_W8>(epilogue, A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
 }
@@ -736,3 +838,22 @@ extern "C" int qvit_gemm_stamps(unsigned long long* host8, int reset) {
   return qvit_hip_status(hipMemcpyFromSymbol(host8, HIP_SYMBOL(qvit_gemm_stamp_sums), 8 * sizeof(unsigned long long)));
 }
 #endif
+
+extern "C" int qvit_gemm_qkv_split(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int wfmt,
+                                   int64_t N, int64_t npad, const float* d_act, const float* d_wt, const float* bias,
+                                   int64_t seq, float in_scale, void* qkv_hi, void* qkv_lo, hipStream_t stream) {
+  if (!A || !Wp || !qkv_hi || !qkv_lo || !d_act || !d_wt) return QVIT_ENULL;
+  if (wfmt != QVIT_W4 && wfmt != QVIT_W8) return QVIT_EINVAL;
+  if (M < 0 || K <= 0 || K % KTILE || lda < K || N <= 0 || N % 64 || npad < N || npad % BN) return QVIT_EINVAL;
+  if (M > INT32_MAX / 2 || npad > INT32_MAX / 2 || K > (1 << 24)) return QVIT_EINVAL;
+  if (seq <= 0 || seq > (1 << 20) || M % seq || !(in_scale > 0.f)) return QVIT_EINVAL;
+  if ((lda % 16) || (((uintptr_t)A) & 15) || (((uintptr_t)Wp) & 15)) return QVIT_EALIGN;
+  if ((((uintptr_t)qkv_hi) & 15) || (((uintptr_t)qkv_lo) & 15)) return QVIT_EALIGN;
+  if (bias && (((uintptr_t)bias) & 15)) return QVIT_EALIGN;
+  if (M == 0) return QVIT_OK;
+  EpiArgs ep{d_act, d_wt, bias, 0, nullptr, nullptr, nullptr, 0, nullptr, (int)seq, 1.0f / (float)seq, in_scale,
+             reinterpret_cast<_Float16*>(qkv_lo)};
+  if (wfmt == QVIT_W4)
+    return launch<QVIT_W4, QVIT_EPI_QKV_SPLIT>(A, M, K, lda, Wp, N, npad, qkv_hi, N, ep, stream);
+  return launch<QVIT_W8, QVIT_EPI_QKV_SPLIT>(A, M, K, lda, Wp, N, npad, qkv_hi, N, ep, stream);
+}

@@ -101,6 +101,11 @@ class ViTAttention(nn.Module):
         return (qkv.is_cuda and qkv.dtype == torch.float32 and self.head_dim == 64 and qkv.dim() == 2
                 and qkv.stride(1) == 1 and not (self.training and self.attn_drop.p > 0))
 
+    def split_ok(self, p_qkv) -> bool:
+        """The fused block can take the split-operand path (qvit_gemm_qkv_split -> qvit_attention_split)."""
+        return (self.head_dim == 64 and p_qkv.n == 3 * self.num_heads * 64
+                and not (self.training and self.attn_drop.p > 0))
+
     def core_hip(self, qkv: torch.Tensor, B: int, N: int, out: torch.Tensor, out_mode: int = _lib.ATT_F32,
                  in_scale: float = 1.0, plan=None) -> torch.Tensor:
         """The same op on the fused HIP kernel (qvit_attention); with out_mode ATT_I8 it also applies the
@@ -221,10 +226,24 @@ class Block(nn.Module):
         codes = torch.empty((M, p_qkv.kpad), dtype=torch.int8, device=x.device)
         _lib.layernorm_quant_i8(x2, self.norm1.weight, self.norm1.bias, self.norm1.eps, p_qkv.qtype, p_qkv.d_act,
                                 p_qkv.qm_act, p_qkv.t_act, 0, codes, p_qkv.kpad)
+        p_proj = a.proj.quant_plan()
+        if a.split_ok(p_qkv):
+            # qkv as pre-scaled fp16 hi/lo head planes, then attention + proj's activation quantizer
+            in_scale = attention_in_scale(p_qkv)
+            hi = torch.empty(M * p_qkv.n, dtype=torch.float16, device=x.device)
+            lo = torch.empty(M * p_qkv.n, dtype=torch.float16, device=x.device)
+            _lib.gemm_qkv_split(codes, M, p_qkv.kpad, p_qkv.packed, p_qkv.wfmt, p_qkv.n, p_qkv.npad, p_qkv.d_act,
+                                p_qkv.d_wt, p_qkv.bias_pad, N, in_scale, hi, lo)
+            codes = torch.empty((M, p_proj.kpad), dtype=torch.int8, device=x.device)
+            if p_proj.kpad != a.num_heads * 64:
+                codes[:, a.num_heads * 64:].zero_()
+            _lib.attention_split(hi, lo, B, N, a.num_heads, 64, a.scale, codes, _lib.ATT_I8, in_scale,
+                                 p_proj.qtype, p_proj.d_act, p_proj.qm_act, p_proj.t_act)
+            a.proj.gemm_codes(codes, p_proj, _lib.EPI_F32_RESID, out=x2)
+            return self._mlp_fused_(x, x2, M)
         qkv = a.qkv.gemm_codes(codes, p_qkv, _lib.EPI_F32)
         if qkv.shape[1] != p_qkv.n:
             qkv = qkv[:, :p_qkv.n]
-        p_proj = a.proj.quant_plan()
         if a.hip_ok(qkv):
             # attention core + proj's activation quantizer in one kernel: int8 codes for the proj GEMM
             codes = torch.empty((M, p_proj.kpad), dtype=torch.int8, device=x.device)
@@ -235,7 +254,11 @@ class Block(nn.Module):
             h = a.core(qkv, B, N).reshape(M, -1)
             codes = a.proj._act_codes(h if h.is_contiguous() else h.contiguous(), p_proj)
         a.proj.gemm_codes(codes, p_proj, _lib.EPI_F32_RESID, out=x2)
-        # x + mlp(norm2(x))
+        return self._mlp_fused_(x, x2, M)
+
+    def _mlp_fused_(self, x: torch.Tensor, x2: torch.Tensor, M: int) -> torch.Tensor:
+        """x + mlp(norm2(x)) in place on the residual buffer."""
+        m = self.mlp
         p_fc1 = m.fc1.quant_plan()
         codes = torch.empty((M, p_fc1.kpad), dtype=torch.int8, device=x.device)
         _lib.layernorm_quant_i8(x2, self.norm2.weight, self.norm2.bias, self.norm2.eps, p_fc1.qtype, p_fc1.d_act,

@@ -110,3 +110,98 @@ def test_attention_argument_validation(dev):
                               None, 0, s) == -1            # int8 mode without quantizer params
     assert lib.qvit_attention(qkv.data_ptr(), 1, 10, 1, 64, 192, 0.125, 0.0, 0, out.data_ptr(), 64, 0, None, None,
                               None, 0, s) == -1            # in_scale must be > 0
+
+
+# ---- split-operand path (qvit_gemm_qkv_split -> qvit_attention_split; the fused block) ----------------
+def split_planes(qkv: torch.Tensor, B: int, N: int, H: int, in_scale: float):
+    """fp16 hi/lo planes [B][3H][N][64] of in_scale * qkv, rounded exactly as the kernels split."""
+    x = qkv[:, :3 * H * 64].float() * in_scale
+    hi = x.half()
+    lo = (x - hi.float()).half()
+    f = lambda t: t.reshape(B, N, 3 * H, 64).permute(0, 2, 1, 3).contiguous().reshape(-1)
+    return f(hi), f(lo)
+
+
+def run_split(dev, B, N, H, qkv, scale, mode=_lib.ATT_F32, in_scale=1.0, **qkw):
+    hi, lo = split_planes(qkv, B, N, H, in_scale)
+    if mode == _lib.ATT_F32:
+        out = torch.full((B * N, H * 64), float("nan"), device=dev)
+    else:
+        out = torch.zeros((B * N, H * 64), dtype=torch.int8, device=dev)
+    _lib.attention_split(hi.to(dev), lo.to(dev), B, N, H, 64, scale, out, mode, in_scale, **qkw)
+    torch.cuda.synchronize()
+    return out.cpu()
+
+
+@pytest.mark.parametrize("B,N,H", [(2, 197, 12), (1, 1, 1), (3, 33, 2), (1, 64, 3), (2, 577, 2), (1, 300, 1),
+                                   (4, 197, 3)])
+def test_attention_split_bitwise_equals_fp32_input_kernel(dev, B, N, H):
+    """Same arithmetic in the same order: the split-input kernel reproduces qvit_attention bit for bit."""
+    g = torch.Generator().manual_seed(N * 5 + H)
+    qkv = torch.randn(B * N, 3 * H * 64, generator=g) * 1.5
+    a = run(dev, B, N, H, qkv, 0.125)
+    b = run_split(dev, B, N, H, qkv, 0.125)
+    assert torch.isfinite(b).all()
+    assert torch.equal(a, b)
+
+
+def test_attention_split_int8_and_in_scale(dev):
+    B, N, H = 2, 197, 12
+    g = torch.Generator().manual_seed(13)
+    qkv = torch.randn(B * N, 3 * H * 64, generator=g)
+    qkv[:, 2 * H * 64:] *= 3.0e4
+    kw = dict(out_qtype=_lib.QT_NONLINEAR, out_d=_p(4e4 ** 0.9 / 127, dev), out_qm=_p(4e4, dev),
+              out_t=_p(0.9, dev))
+    a = run(dev, B, N, H, qkv, 0.125, mode=_lib.ATT_I8, in_scale=2.0 ** -2, **kw)
+    b = run_split(dev, B, N, H, qkv, 0.125, mode=_lib.ATT_I8, in_scale=2.0 ** -2, **kw)
+    assert torch.equal(a, b)
+    assert len(torch.unique(b)) > 50
+
+
+@pytest.mark.parametrize("wfmt", [_lib.W4, _lib.W8])
+@pytest.mark.parametrize("seq,B", [(197, 3), (50, 7), (1, 130)])
+def test_gemm_qkv_split_equals_f32_epilogue(dev, wfmt, seq, B):
+    """hi/lo planes are the exact split of in_scale times the QVIT_EPI_F32 output, head-major."""
+    from test_gpu_kernels import act_buffer, pack_codes
+    H = 4
+    M, N, K = B * seq, 3 * H * 64, 384
+    g = torch.Generator().manual_seed(seq + B + wfmt)
+    a = torch.randint(-127, 128, (M, K), generator=g)
+    lim = 7 if wfmt == _lib.W4 else 127
+    w = torch.randint(-lim, lim + 1, (N, K), generator=g)
+    bias = torch.randn(N, generator=g)
+    packed, npad, kpad = pack_codes(w, wfmt, dev)
+    bias_pad = _lib.pad_bias(bias.to(dev), N, npad, dev)
+    A = act_buffer(a, kpad, dev)
+    da, dw = _p(0.01, dev), _p(0.003, dev)
+    ref = torch.empty((M, N), device=dev)
+    _lib.gemm(A, M, kpad, packed, wfmt, N, npad, da, dw, bias_pad, _lib.EPI_F32, ref)
+    s = 2.0 ** -3
+    hi = torch.full((M * N,), float("nan"), dtype=torch.float16, device=dev)
+    lo = torch.full((M * N,), float("nan"), dtype=torch.float16, device=dev)
+    _lib.gemm_qkv_split(A, M, kpad, packed, wfmt, N, npad, da, dw, bias_pad, seq, s, hi, lo)
+    torch.cuda.synchronize()
+    whi, wlo = split_planes(ref.cpu(), B, seq, H, s)
+    assert torch.equal(hi.cpu(), whi) and torch.equal(lo.cpu(), wlo)
+
+
+def test_split_argument_validation(dev):
+    lib = _lib.load()
+    s = torch.cuda.current_stream().cuda_stream
+    buf = torch.zeros(4096, dtype=torch.float16, device=dev)
+    out = torch.zeros(10, 64, device=dev)
+    p = buf.data_ptr()
+    assert lib.qvit_attention_split(p, p, 1, 10, 1, 32, 0.125, 1.0, 0, out.data_ptr(), 64, 0, None, None, None, 0,
+                                    s) == -1          # head_dim
+    assert lib.qvit_attention_split(p, None, 1, 10, 1, 64, 0.125, 1.0, 0, out.data_ptr(), 64, 0, None, None, None,
+                                    0, s) == -3       # NULL lo plane
+    assert lib.qvit_attention_split(p + 2, p, 1, 10, 1, 64, 0.125, 1.0, 0, out.data_ptr(), 64, 0, None, None, None,
+                                    0, s) == -2       # misaligned
+    one = _p(1.0, dev).data_ptr()
+    # N % 64, M % seq, in_scale
+    assert lib.qvit_gemm_qkv_split(p, 10, 128, 128, p, 4, 96, 256, one, one, None, 10, 1.0, p, p, s) == -1
+    assert lib.qvit_gemm_qkv_split(p, 10, 128, 128, p, 4, 192, 256, one, one, None, 3, 1.0, p, p, s) == -1
+    assert lib.qvit_gemm_qkv_split(p, 10, 128, 128, p, 4, 192, 256, one, one, None, 10, 0.0, p, p, s) == -1
+    # qvit_gemm does not accept the split epilogue
+    assert lib.qvit_gemm(p, 10, 128, 128, p, 4, 192, 256, one, one, None, 5, p, 192, 0, None, None, None, 0, None,
+                         s) == -1

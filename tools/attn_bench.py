@@ -30,7 +30,11 @@ def main():
     ap.add_argument("--N", type=int, default=197)
     ap.add_argument("--H", type=int, default=12)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--lib", default="", help="load this library build instead (diagnostic variants)")
+    ap.add_argument("--split-only", action="store_true")
     a = ap.parse_args()
+    if a.lib:
+        _lib.load(a.lib)
     dev = torch.device("cuda:0")
     B, N, H = a.B, a.N, a.H
     qkv = torch.randn(B * N, 3 * H * 64, device=dev)
@@ -44,11 +48,20 @@ def main():
         at = ((x[0] @ x[1].transpose(-2, -1)) * 0.125).softmax(dim=-1)
         return (at @ x[2]).transpose(1, 2).reshape(B * N, H * 64)
 
+    hi = qkv.half().reshape(-1)
+    lo = (qkv - qkv.half().float()).half().reshape(-1)
+    sp = timeit(lambda: _lib.attention_split(hi, lo, B, N, H, 64, 0.125, codes, _lib.ATT_I8, 1.0, _lib.QT_NONLINEAR,
+                                             d, qm, t), a.iters)
+    spf = timeit(lambda: _lib.attention_split(hi, lo, B, N, H, 64, 0.125, out), a.iters)
+    flops = 4.0 * B * H * N * N * 64
+    print(f"{'split i8':20s} {sp*1e3:9.1f} us  {flops/sp/1e9:8.1f} TFLOP/s (fp32-equivalent)", flush=True)
+    print(f"{'split f32':20s} {spf*1e3:9.1f} us  {flops/spf/1e9:8.1f} TFLOP/s (fp32-equivalent)", flush=True)
+    if a.split_only:
+        return
     f32 = timeit(lambda: _lib.attention(qkv, B, N, H, 64, 0.125, out), a.iters)
     i8 = timeit(lambda: _lib.attention(qkv, B, N, H, 64, 0.125, codes, _lib.ATT_I8, 1.0, _lib.QT_NONLINEAR, d, qm, t),
                 a.iters)
     tr = timeit(torch_ref, a.iters)
-    flops = 4.0 * B * H * N * N * 64
     for name, ms in (("qvit_attention f32", f32), ("qvit_attention i8", i8), ("torch fp32", tr)):
         print(f"{name:20s} {ms*1e3:9.1f} us  {flops/ms/1e9:8.1f} TFLOP/s (fp32-equivalent)", flush=True)
 
