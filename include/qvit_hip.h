@@ -263,11 +263,13 @@ int qvit_gemm_qkv_split(const int8_t* A, int64_t M, int64_t K, int64_t lda,
 /*
  * qvit_attention on the split operands of qvit_gemm_qkv_split (planes [B][3H][N][64], in_scale the
  * same power of two): identical arithmetic; K/V blocks stream into LDS by DMA with no conversion.
+ * epi_table (QVIT_ATT_I8 only, nullable): a qvit_epi_table_build table with QVIT_EPI_I8 semantics for
+ * the output quantizer (<= 2046 buckets; used only if valid, results never depend on it).
  */
 int qvit_attention_split(const void* qkv_hi, const void* qkv_lo, int64_t B, int64_t N, int64_t H,
                          int64_t head_dim, float scale, float in_scale, int out_mode, void* out,
                          int64_t ldo, int out_qtype, const float* out_d, const float* out_qm,
-                         const float* out_t, int out_levels, hipStream_t stream);
+                         const float* out_t, int out_levels, const void* epi_table, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -73,7 +73,7 @@ _SIGNATURES = {
     "qvit_gemm_qkv_split": [_c_p, _i64, _i64, _i64, _c_p, _i32, _i64, _i64, _c_p, _c_p, _c_p, _i64, _f32, _c_p,
                             _c_p, _c_p],
     "qvit_attention_split": [_c_p, _c_p, _i64, _i64, _i64, _i64, _f32, _f32, _i32, _c_p, _i64, _i32, _c_p, _c_p,
-                             _c_p, _i32, _c_p],
+                             _c_p, _i32, _c_p, _c_p],
 }
 STRING_FUNCS = {"qvit_strerror": [_i32], "qvit_version": []}
 EXPORTED_SYMBOLS = sorted(list(_SIGNATURES) + list(STRING_FUNCS))
@@ -243,14 +243,16 @@ def gemm_qkv_split(A: torch.Tensor, M: int, K: int, packed: torch.Tensor, wfmt: 
 
 def attention_split(hi: torch.Tensor, lo: torch.Tensor, B: int, N: int, H: int, head_dim: int, scale: float,
                     out: torch.Tensor, out_mode: int = ATT_F32, in_scale: float = 1.0, out_qtype: int = 0,
-                    out_d=None, out_qm=None, out_t=None, out_levels: int = 0) -> torch.Tensor:
-    """qvit_attention on the split planes of gemm_qkv_split."""
+                    out_d=None, out_qm=None, out_t=None, out_levels: int = 0,
+                    epi_table: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """qvit_attention on the split planes of gemm_qkv_split (epi_table: EPI_I8 code table of the output
+    quantizer, optional)."""
     _require_gpu(hi, "qkv_hi")
     assert hi.dtype == torch.float16 and lo.dtype == torch.float16
     assert hi.numel() >= B * 3 * H * N * head_dim and lo.numel() >= B * 3 * H * N * head_dim
     _check(load().qvit_attention_split(_ptr(hi), _ptr(lo), B, N, H, head_dim, scale, in_scale, out_mode, _ptr(out),
                                        out.stride(0), out_qtype, _ptr(out_d), _ptr(out_qm), _ptr(out_t), out_levels,
-                                       _stream(hi.device)), "qvit_attention_split")
+                                       _ptr(epi_table), _stream(hi.device)), "qvit_attention_split")
     return out
 
 

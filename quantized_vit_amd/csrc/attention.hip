@@ -184,26 +184,68 @@ QVIT_DEV void attend_n(int nt, bool mask, const int8_t* st, const h8 (&qh)[QTW][
   attend(nt, mask, st, qh, ql, m, l, o, koffs, voffs, kbase, N, sl2);
 }
 
-// Normalise and write a wave's query tiles: fp32 rows, or the next layer's int8 codes.
+// The int8 epilogue's code table in LDS (qvit_epi_table_build with QVIT_EPI_I8 semantics), if any.
+struct EpiLds {
+  const int8_t* ent;  // entries (header excluded), nullptr -> per-element quantizer
+  float c0, inv_w, nbm1;
+};
+
+// 4x4 transpose between the lane groups g (lanes 16g..16g+15) and the 4 registers: afterwards lane g
+// holds what lane k held in register g, as w[k] (two permlane32 swaps, then two permlane16 swaps).
+QVIT_DEV void transpose_groups(uint32_t (&w)[4]) {
+  auto a = __builtin_amdgcn_permlane32_swap(w[0], w[2], false, false);
+  auto b = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
+  w[0] = a[0]; w[2] = a[1]; w[1] = b[0]; w[3] = b[1];
+  auto c = __builtin_amdgcn_permlane16_swap(w[0], w[1], false, false);
+  auto d = __builtin_amdgcn_permlane16_swap(w[2], w[3], false, false);
+  w[0] = c[0]; w[1] = c[1]; w[2] = d[0]; w[3] = d[1];
+}
+
+// Normalise and write a wave's query tiles: fp32 rows, or the next layer's int8 codes. With st16 the
+// codes of a row leave as one 16-B store per lane (lane group g: columns 16g .. 16g+15 of the head).
 template <int OUT>
 QVIT_DEV void attend_store(const bool (&tv)[QTW], const float (&l)[QTW], const f4 (&o)[QTW][4], int qtile0, int q0,
-                           int N, int b, int h, float in_scale, void* out, int64_t ldo, const QParams& qp) {
+                           int N, int b, int h, float in_scale, void* out, int64_t ldo, const QParams& qp,
+                           const EpiLds& tb, bool st16) {
   const int lane = threadIdx.x & 63;
   const int fr = lane & 15, g = lane >> 4;
 #pragma unroll
   for (int i = 0; i < QTW; ++i) {
-    if (!tv[i]) continue;
+    if (!tv[i]) continue;  // wave-uniform
     const float inv = 1.f / (xsum(l[i]) * in_scale);
     const int q = q0 + 16 * (qtile0 + NWAVES * i) + fr;
-    if (q >= N) continue;
     const int64_t row = (int64_t)b * N + q;
+    if (OUT == 0) {
+      if (q >= N) continue;
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const int col = h * HD + 16 * dt + 4 * g;
-      f4 v = o[i][dt] * inv;
-      if (OUT == 0) {
-        *reinterpret_cast<f4*>(reinterpret_cast<float*>(out) + row * ldo + col) = v;
-      } else {
+      for (int dt = 0; dt < 4; ++dt) {
+        const int col = h * HD + 16 * dt + 4 * g;
+        *reinterpret_cast<f4*>(reinterpret_cast<float*>(out) + row * ldo + col) = o[i][dt] * inv;
+      }
+      continue;
+    }
+    uint32_t wd[4];
+    if (tb.ent != nullptr) {
+      float v[4][4];
+      uint2 e[4][4];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[dt][j] = o[i][dt][j] * inv;
+          e[dt][j] = *reinterpret_cast<const uint2*>(tb.ent + (epi_bucket(v[dt][j], tb.c0, tb.inv_w, tb.nbm1) << 3));
+        }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        epi_select_byte<0>(wd[dt], v[dt][0], __uint_as_float(e[dt][0].x), e[dt][0].y);
+        epi_select_byte<1>(wd[dt], v[dt][1], __uint_as_float(e[dt][1].x), e[dt][1].y);
+        epi_select_byte<2>(wd[dt], v[dt][2], __uint_as_float(e[dt][2].x), e[dt][2].y);
+        epi_select_byte<3>(wd[dt], v[dt][3], __uint_as_float(e[dt][3].x), e[dt][3].y);
+      }
+    } else {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const f4 v = o[i][dt] * inv;
         float k[4];
         bool need[4];
 #pragma unroll
@@ -216,8 +258,16 @@ QVIT_DEV void attend_store(const bool (&tv)[QTW], const float (&l)[QTW], const f
         uint32_t word = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) word |= ((uint32_t)(uint8_t)to_i8_sat(k[j])) << (8 * j);
-        *reinterpret_cast<uint32_t*>(reinterpret_cast<int8_t*>(out) + row * ldo + col) = word;
+        wd[dt] = word;
       }
+    }
+    int8_t* dst = reinterpret_cast<int8_t*>(out) + row * ldo + h * HD;
+    if (st16) {
+      transpose_groups(wd);
+      if (q < N) *reinterpret_cast<uint4*>(dst + 16 * g) = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+    } else if (q < N) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) *reinterpret_cast<uint32_t*>(dst + 16 * dt + 4 * g) = wd[dt];
     }
   }
 }
@@ -344,7 +394,8 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const float* __restrict__ 
   }
   QParams qp{};
   if (OUT == 1) qp = load_qparams(out_qtype, out_d, out_qm, out_t, out_levels);
-  attend_store<OUT>(tv, l, o, wave, q0, N, b, h, in_scale, out, ldo, qp);
+  const bool st16 = ((ldo & 15) == 0) && ((((uintptr_t)out) & 15) == 0);
+  attend_store<OUT>(tv, l, o, wave, q0, N, b, h, in_scale, out, ldo, qp, EpiLds{nullptr, 0.f, 0.f, 0.f}, st16);
 }
 
 // ---- split fp16 input (the fused block path) --------------------------------------------------------
@@ -386,14 +437,16 @@ QVIT_DEV void block_sync() {
 // before the stream starts), so the only vmcnt waits are the counted stage waits; the output stores of a
 // unit's epilogue do join the count and are drained by the next wait.
 constexpr int QB = 64;  // queries per query block
+constexpr int TBL_BYTES = 16384;  // int8 epilogue code table (<= 2046 buckets): 2 x (64 + 16) KiB per CU
 
 template <int OUT>
 __global__ __launch_bounds__(256, 2) void attn_split_kernel(const _Float16* __restrict__ hi,
                                                             const _Float16* __restrict__ lo, int N, int H, int nunits,
                                                             float scale, float in_scale, void* __restrict__ out,
                                                             int64_t ldo, int out_qtype, const float* out_d,
-                                                            const float* out_qm, const float* out_t, int out_levels) {
-  __shared__ __attribute__((aligned(16))) int8_t smem[SRING * STAGE];
+                                                            const float* out_qm, const float* out_t, int out_levels,
+                                                            const int8_t* __restrict__ epi_table) {
+  __shared__ __attribute__((aligned(16))) int8_t smem[SRING * STAGE + (OUT == 1 ? TBL_BYTES : 0)];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -401,8 +454,21 @@ __global__ __launch_bounds__(256, 2) void attn_split_kernel(const _Float16* __re
   const int g = lane >> 4;
 
   QParams qp{};
-  if (OUT == 1) qp = load_qparams(out_qtype, out_d, out_qm, out_t, out_levels);
+  EpiLds tb{nullptr, 0.f, 0.f, 0.f};
+  if (OUT == 1) {
+    qp = load_qparams(out_qtype, out_d, out_qm, out_t, out_levels);
+    if (epi_table != nullptr) {  // the code table -> LDS, once per workgroup
+      const EpiTableHdr hd = *reinterpret_cast<const EpiTableHdr*>(epi_table);
+      if (hd.valid != 0 && hd.nb >= 1 && 16 + 8 * hd.nb <= TBL_BYTES) {
+        int8_t* tl = smem + SRING * STAGE;
+        for (int k = tid; k < (16 + 8 * hd.nb + 15) / 16; k += 256)
+          reinterpret_cast<uint4*>(tl)[k] = reinterpret_cast<const uint4*>(epi_table)[k];
+        tb = EpiLds{tl + sizeof(EpiTableHdr), hd.c0, hd.inv_w, (float)(hd.nb - 1)};
+      }
+    }
+  }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): nothing of the compiler's own is pending below
+  const bool st16 = ((ldo & 15) == 0) && ((((uintptr_t)out) & 15) == 0);
 
   const int ngroups = (N + QG - 1) / QG;
   const int nqb = (N < QG ? (N + QB - 1) / QB : QG / QB);
@@ -509,7 +575,7 @@ __global__ __launch_bounds__(256, 2) void attn_split_kernel(const _Float16* __re
     bool tv[QTW];
 #pragma unroll
     for (int i = 0; i < QTW; ++i) tv[i] = i < nt;
-    attend_store<OUT>(tv, l, o, wr, q0, N, b, h, in_scale, out, ldo, qp);
+    attend_store<OUT>(tv, l, o, wr, q0, N, b, h, in_scale, out, ldo, qp, tb, st16);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -551,8 +617,10 @@ extern "C" int qvit_attention(const float* qkv, int64_t B, int64_t N, int64_t H,
 extern "C" int qvit_attention_split(const void* qkv_hi, const void* qkv_lo, int64_t B, int64_t N, int64_t H,
                                     int64_t head_dim, float scale, float in_scale, int out_mode, void* out,
                                     int64_t ldo, int out_qtype, const float* out_d, const float* out_qm,
-                                    const float* out_t, int out_levels, hipStream_t stream) {
+                                    const float* out_t, int out_levels, const void* epi_table,
+                                    hipStream_t stream) {
   if (!qkv_hi || !qkv_lo || !out) return QVIT_ENULL;
+  if (epi_table && (((uintptr_t)epi_table) & 15)) return QVIT_EALIGN;
   if (head_dim != HD) return QVIT_EINVAL;
   if (B < 0 || N <= 0 || H <= 0 || ldo < H * HD) return QVIT_EINVAL;
   if (B * N > INT32_MAX || N > (1 << 20) || !(in_scale > 0.f)) return QVIT_EINVAL;
@@ -583,9 +651,11 @@ extern "C" int qvit_attention_split(const void* qkv_hi, const void* qkv_lo, int6
   const int64_t grid = std::min<int64_t>(nblk, 2 * (int64_t)cus);  // two resident workgroups per CU
   if (out_mode == QVIT_ATT_F32)
     hipLaunchKernelGGL(attn_split_kernel<0>, dim3((unsigned)grid), dim3(256), 0, stream, hi, lo, (int)N, (int)H,
-                       (int)nblk, scale, in_scale, out, ldo, out_qtype, out_d, out_qm, out_t, out_levels);
+                       (int)nblk, scale, in_scale, out, ldo, out_qtype, out_d, out_qm, out_t, out_levels,
+                       nullptr);
   else
     hipLaunchKernelGGL(attn_split_kernel<1>, dim3((unsigned)grid), dim3(256), 0, stream, hi, lo, (int)N, (int)H,
-                       (int)nblk, scale, in_scale, out, ldo, out_qtype, out_d, out_qm, out_t, out_levels);
+                       (int)nblk, scale, in_scale, out, ldo, out_qtype, out_d, out_qm, out_t, out_levels,
+                       reinterpret_cast<const int8_t*>(epi_table));
   return qvit_hip_status(hipGetLastError());
 }

@@ -143,44 +143,6 @@ struct EpiArgs {
 // then still reads the right code). The table is built on the device by bisection with the very same F
 // the direct epilogue evaluates, and validated (both ends constant, no bucket whose end codes differ
 // by more than one); an invalid table makes the epilogue fall back to the direct computation.
-struct EpiTableHdr {
-  float c0;     // -v_lo * inv_w (rounded): bucket(v) = clamp(int(fma(v, inv_w, c0)), 0, nb - 1)
-  float inv_w;
-  int nb;
-  int valid;
-};
-struct EpiTableEnt {
-  float thr;
-  int8_t lo, hi;
-  int16_t pad;
-};
-// Monotone in v (the bisection in the builder relies on it); one FMA and one med3 in the epilogue.
-QVIT_DEV int epi_bucket(float v, float c0, float inv_w, float nbm1) {
-  return (int)__builtin_amdgcn_fmed3f(fmaf(v, inv_w, c0), 0.f, nbm1);
-}
-
-// wd.byte[J] = (v >= thr) ? byte 1 of lohi : byte 0 of lohi (J = 0 also zeroes bytes 1..3):
-// a v_cmp and one SDWA v_cndmask that writes the selected byte in place.
-template <int J>
-QVIT_DEV void epi_select_byte(uint32_t& wd, float v, float thr, uint32_t lohi) {
-  if (J == 0)
-    asm("v_cmp_ge_f32_e32 vcc, %1, %2\n\t"
-        "v_cndmask_b32_sdwa %0, %3, %3, vcc dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:BYTE_1"
-        : "=v"(wd) : "v"(v), "v"(thr), "v"(lohi) : "vcc");
-  else if (J == 1)
-    asm("v_cmp_ge_f32_e32 vcc, %1, %2\n\t"
-        "v_cndmask_b32_sdwa %0, %3, %3, vcc dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_0 src1_sel:BYTE_1"
-        : "+v"(wd) : "v"(v), "v"(thr), "v"(lohi) : "vcc");
-  else if (J == 2)
-    asm("v_cmp_ge_f32_e32 vcc, %1, %2\n\t"
-        "v_cndmask_b32_sdwa %0, %3, %3, vcc dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_0 src1_sel:BYTE_1"
-        : "+v"(wd) : "v"(v), "v"(thr), "v"(lohi) : "vcc");
-  else
-    asm("v_cmp_ge_f32_e32 vcc, %1, %2\n\t"
-        "v_cndmask_b32_sdwa %0, %3, %3, vcc dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_0 src1_sel:BYTE_1"
-        : "+v"(wd) : "v"(v), "v"(thr), "v"(lohi) : "vcc");
-}
-
 QVIT_DEV float epi_F(float v, int gelu, const QParams& qp) { return quant_code(gelu ? gelu_ref(v) : v, qp); }
 
 // float <-> totally ordered int key (for bisection over representable floats)

@@ -26,7 +26,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
-from .quant_layers import QuantizationMode, QuantizeConv2d, QuantizeLinear
+from .quant_layers import QuantizationMode, QuantizeConv2d, QuantizeLinear, epilogue_table
 
 # Benchmark instrumentation: when KERNEL_TIMING["fc1"] is a list, the fused block appends a
 # (start, end) HIP event pair recorded on the launch stream around every fc1 GEMM launch.
@@ -238,7 +238,8 @@ class Block(nn.Module):
             if p_proj.kpad != a.num_heads * 64:
                 codes[:, a.num_heads * 64:].zero_()
             _lib.attention_split(hi, lo, B, N, a.num_heads, 64, a.scale, codes, _lib.ATT_I8, in_scale,
-                                 p_proj.qtype, p_proj.d_act, p_proj.qm_act, p_proj.t_act)
+                                 p_proj.qtype, p_proj.d_act, p_proj.qm_act, p_proj.t_act,
+                                 epi_table=epilogue_table(p_proj, _lib.EPI_I8))
             a.proj.gemm_codes(codes, p_proj, _lib.EPI_F32_RESID, out=x2)
             return self._mlp_fused_(x, x2, M)
         qkv = a.qkv.gemm_codes(codes, p_qkv, _lib.EPI_F32)

@@ -192,11 +192,13 @@ def test_split_argument_validation(dev):
     out = torch.zeros(10, 64, device=dev)
     p = buf.data_ptr()
     assert lib.qvit_attention_split(p, p, 1, 10, 1, 32, 0.125, 1.0, 0, out.data_ptr(), 64, 0, None, None, None, 0,
-                                    s) == -1          # head_dim
+                                    None, s) == -1    # head_dim
     assert lib.qvit_attention_split(p, None, 1, 10, 1, 64, 0.125, 1.0, 0, out.data_ptr(), 64, 0, None, None, None,
-                                    0, s) == -3       # NULL lo plane
+                                    0, None, s) == -3  # NULL lo plane
     assert lib.qvit_attention_split(p + 2, p, 1, 10, 1, 64, 0.125, 1.0, 0, out.data_ptr(), 64, 0, None, None, None,
-                                    0, s) == -2       # misaligned
+                                    0, None, s) == -2  # misaligned
+    assert lib.qvit_attention_split(p, p, 1, 10, 1, 64, 0.125, 1.0, 0, out.data_ptr(), 64, 0, None, None, None,
+                                    0, p + 4, s) == -2  # misaligned code table
     one = _p(1.0, dev).data_ptr()
     # N % 64, M % seq, in_scale
     assert lib.qvit_gemm_qkv_split(p, 10, 128, 128, p, 4, 96, 256, one, one, None, 10, 1.0, p, p, s) == -1
@@ -205,3 +207,33 @@ def test_split_argument_validation(dev):
     # qvit_gemm does not accept the split epilogue
     assert lib.qvit_gemm(p, 10, 128, 128, p, 4, 192, 256, one, one, None, 5, p, 192, 0, None, None, None, 0, None,
                          s) == -1
+
+
+@pytest.mark.parametrize("qt,t", [(O.LINEAR, 1.0), (O.NONLINEAR, 1.0), (O.NONLINEAR, 0.8)])
+@pytest.mark.parametrize("ldo", [12 * 64, 12 * 64 + 4])
+def test_attention_split_code_table_equals_direct(dev, qt, t, ldo):
+    """The int8 epilogue through the quantizer's code table (and the 16-B transposed stores, ldo % 16 == 0)
+    writes exactly the codes of the per-element quantizer (and of the fp32-input kernel)."""
+    from quantized_vit_amd.quant_layers import epilogue_table_geometry, saturation_level
+    B, N, H = 3, 197, 12
+    g = torch.Generator().manual_seed(17 + ldo)
+    qkv = torch.randn(B * N, 3 * H * 64, generator=g)
+    d, qm = 0.9 / 127, 0.9
+    if qt == O.NONLINEAR:
+        d = qm ** t / 127
+    qtc = _lib.QT_LINEAR if qt == O.LINEAR else _lib.QT_NONLINEAR
+    kw = dict(out_qtype=qtc, out_d=_p(d, dev), out_qm=_p(qm, dev), out_t=_p(t, dev) if qt == O.NONLINEAR else None)
+    geo = epilogue_table_geometry(qtc, d, qm, t, saturation_level(qtc, d, qm, t), False)
+    table = _lib.epi_table_build(_lib.EPI_I8, qtc, kw["out_d"], kw["out_qm"], kw["out_t"], 0, *geo, dev)
+    assert int(table[12:16].view(torch.int32).item()) == 1
+    hi, lo = split_planes(qkv, B, N, H, 1.0)
+    outs = []
+    for tab in (None, table):
+        out = torch.zeros((B * N, ldo), dtype=torch.int8, device=dev)
+        _lib.attention_split(hi.to(dev), lo.to(dev), B, N, H, 64, 0.125, out, _lib.ATT_I8, 1.0, epi_table=tab, **kw)
+        torch.cuda.synchronize()
+        outs.append(out.cpu())
+    ref = run(dev, B, N, H, qkv, 0.125, mode=_lib.ATT_I8, **kw)
+    assert torch.equal(outs[0][:, :H * 64], ref) and torch.equal(outs[1][:, :H * 64], ref)
+    assert (outs[1][:, H * 64:] == 0).all()
+    assert len(torch.unique(ref)) > 100
