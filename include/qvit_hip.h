@@ -150,12 +150,15 @@ int qvit_im2col_quant_i8(const float* x, int64_t B, int64_t C, int64_t H, int64_
  * LayerNorm (biased variance, eps) followed by the next layer's activation quantizer.
  *   x : fp32 [rows][ldx] (D = cols), gamma/beta fp32 [cols] (may be NULL -> 1 / 0)
  *   codes : int8 [rows][ldc], columns [cols, kpad) zero.
+ *   code_table : nullable, 16-B aligned; a qvit_epi_table_build table (QVIT_EPI_I8 semantics) of the
+ *            same quantizer, used only if valid and <= 2046 buckets (results never depend on it).
  */
 int qvit_layernorm_quant_i8(const float* x, int64_t rows, int64_t cols, int64_t ldx,
                             const float* gamma, const float* beta, float eps,
                             int qtype, const float* d_quant, const float* q_m,
                             const float* t_quant, int levels,
-                            int8_t* codes, int64_t ldc, int64_t kpad, hipStream_t stream);
+                            int8_t* codes, int64_t ldc, int64_t kpad,
+                            const void* code_table, hipStream_t stream);
 
 /*
  * Quantized contraction C = epilogue(A_codes @ W_codes^T).

@@ -58,7 +58,7 @@ _SIGNATURES = {
     "qvit_im2col_quant_i8": [_c_p, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32,
                              _i32, _c_p, _c_p, _c_p, _i32, _c_p, _i64, _i64, _c_p],
     "qvit_layernorm_quant_i8": [_c_p, _i64, _i64, _i64, _c_p, _c_p, _f32, _i32, _c_p, _c_p, _c_p, _i32,
-                                _c_p, _i64, _i64, _c_p],
+                                _c_p, _i64, _i64, _c_p, _c_p],
     "qvit_gemm": [_c_p, _i64, _i64, _i64, _c_p, _i32, _i64, _i64, _c_p, _c_p, _c_p, _i32, _c_p, _i64,
                   _i32, _c_p, _c_p, _c_p, _i32, _c_p, _c_p],
     "qvit_epi_table_build": [_i32, _i32, _c_p, _c_p, _c_p, _i32, _f32, _f32, _i64, _c_p, _c_p],
@@ -186,13 +186,15 @@ def im2col_quant_i8(x: torch.Tensor, kh: int, kw: int, sh: int, sw: int, ph: int
 
 
 def layernorm_quant_i8(x2d: torch.Tensor, gamma: Optional[torch.Tensor], beta: Optional[torch.Tensor], eps: float,
-                       qtype: int, d, qm, t, levels: int, out: torch.Tensor, kpad: int) -> torch.Tensor:
+                       qtype: int, d, qm, t, levels: int, out: torch.Tensor, kpad: int,
+                       code_table: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """LayerNorm + activation quantizer -> int8 codes (code_table: EPI_I8 table of the quantizer, optional)."""
     _require_gpu(x2d, "input")
     assert x2d.dtype == torch.float32 and x2d.stride(1) == 1
     rows, cols = x2d.shape
     _check(load().qvit_layernorm_quant_i8(_ptr(x2d), rows, cols, x2d.stride(0), _ptr(gamma), _ptr(beta), eps, qtype,
                                           _ptr(d), _ptr(qm), _ptr(t), levels, _ptr(out), out.stride(0), kpad,
-                                          _stream(x2d.device)), "qvit_layernorm_quant_i8")
+                                          _ptr(code_table), _stream(x2d.device)), "qvit_layernorm_quant_i8")
     return out
 
 

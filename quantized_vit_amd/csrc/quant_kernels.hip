@@ -5,6 +5,8 @@
 // allows), so the bound is HBM bandwidth: 5 bytes moved per element.
 #include "qvit_common.h"
 
+#include <algorithm>
+
 namespace {
 
 constexpr int kThreads = 256;
@@ -280,6 +282,117 @@ __global__ __launch_bounds__(kThreads) void layernorm_quant_reg_kernel(
   for (int64_t c = cols + lane; c < kpad; c += 64) cr[c] = 0;
 }
 
+// The same butterfly (xor 32, 16, 8, 4, 2, 1; identical sums in every lane) with the exact-xor steps on
+// permlane swaps and DPP instead of LDS shuffles.
+QVIT_DEV float wave_sum_fast(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(b[0]) + __uint_as_float(b[1]);
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));  // row_ror:8
+  v += __shfl_xor(v, 4, 64);
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xf, 0xf, false));   // xor 2
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xf, 0xf, false));   // xor 1
+  return v;
+}
+
+// Persistent register-resident LayerNorm + quantizer (cols % 4 == 0, cols <= 256 * NV): each wave walks
+// rows wave, wave + nwaves, ... with the next row's load in flight while the current row is finished;
+// gamma/beta, the quantizer scalars and the code table (QVIT_EPI_I8 semantics, nullable) are read once
+// per workgroup. Same arithmetic as layernorm_quant_reg_kernel, row for row.
+constexpr int LN_TBL_BYTES = 16384;
+template <int NV>
+__global__ __launch_bounds__(kThreads) void layernorm_quant_persist_kernel(
+    const float* __restrict__ x, int64_t rows, int64_t cols, int64_t ldx, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, int qtype, const float* d, const float* qm, const float* t,
+    int levels, int8_t* __restrict__ codes, int64_t ldc, int64_t kpad, const int8_t* __restrict__ table) {
+  __shared__ __attribute__((aligned(16))) int8_t tl[LN_TBL_BYTES];
+  const QParams p = load_qparams(qtype, d, qm, t, levels);
+  const int lane = threadIdx.x & 63;
+  const int tid = threadIdx.x;
+  const int8_t* ent = nullptr;
+  float c0 = 0.f, inv_w = 0.f, nbm1 = 0.f;
+  if (table != nullptr) {
+    const EpiTableHdr hd = *reinterpret_cast<const EpiTableHdr*>(table);
+    if (hd.valid != 0 && hd.nb >= 1 && 16 + 8 * hd.nb <= LN_TBL_BYTES) {
+      for (int k = tid; k < (16 + 8 * hd.nb + 15) / 16; k += kThreads)
+        reinterpret_cast<uint4*>(tl)[k] = reinterpret_cast<const uint4*>(table)[k];
+      ent = tl + sizeof(EpiTableHdr);
+      c0 = hd.c0;
+      inv_w = hd.inv_w;
+      nbm1 = (float)(hd.nb - 1);
+    }
+  }
+  __syncthreads();
+  float4 gv[NV], bv[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int64_t c = 4 * (lane + 64 * i);
+    gv[i] = (gamma && c < cols) ? *reinterpret_cast<const float4*>(gamma + c) : make_float4(1.f, 1.f, 1.f, 1.f);
+    bv[i] = (beta && c < cols) ? *reinterpret_cast<const float4*>(beta + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const int64_t nwaves = ((int64_t)gridDim.x * kThreads) >> 6;
+  int64_t r = (blockIdx.x * (int64_t)kThreads + tid) >> 6;
+  float4 v[NV];
+  auto load_row = [&](int64_t rr, float4 (&dst)[NV]) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int64_t c = 4 * (lane + 64 * i);
+      dst[i] = (rr < rows && c < cols) ? *reinterpret_cast<const float4*>(x + rr * ldx + c)
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  load_row(r, v);
+  for (; r < rows; r += nwaves) {
+    float4 vn[NV];
+    load_row(r + nwaves, vn);
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    const float mean = wave_sum_fast(s) / (float)cols;
+    float s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int64_t c = 4 * (lane + 64 * i);
+      if (c < cols) {
+        const float a = v[i].x - mean, b = v[i].y - mean, cc = v[i].z - mean, dd = v[i].w - mean;
+        s2 += (a * a + b * b) + (cc * cc + dd * dd);
+      }
+    }
+    const float var = wave_sum_fast(s2) / (float)cols;
+    const float rstd = 1.0f / sqrtf(var + eps);
+    int8_t* cr = codes + r * ldc;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int64_t c = 4 * (lane + 64 * i);
+      if (c < cols) {
+        const float y[4] = {(v[i].x - mean) * rstd * gv[i].x + bv[i].x, (v[i].y - mean) * rstd * gv[i].y + bv[i].y,
+                            (v[i].z - mean) * rstd * gv[i].z + bv[i].z, (v[i].w - mean) * rstd * gv[i].w + bv[i].w};
+        uint32_t word;
+        if (ent != nullptr) {
+          uint2 e[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            e[j] = *reinterpret_cast<const uint2*>(ent + (epi_bucket(y[j], c0, inv_w, nbm1) << 3));
+          epi_select_byte<0>(word, y[0], __uint_as_float(e[0].x), e[0].y);
+          epi_select_byte<1>(word, y[1], __uint_as_float(e[1].x), e[1].y);
+          epi_select_byte<2>(word, y[2], __uint_as_float(e[2].x), e[2].y);
+          epi_select_byte<3>(word, y[3], __uint_as_float(e[3].x), e[3].y);
+        } else {
+          word = (uint32_t)(uint8_t)to_i8_sat(quant_code(y[0], p)) |
+                 ((uint32_t)(uint8_t)to_i8_sat(quant_code(y[1], p)) << 8) |
+                 ((uint32_t)(uint8_t)to_i8_sat(quant_code(y[2], p)) << 16) |
+                 ((uint32_t)(uint8_t)to_i8_sat(quant_code(y[3], p)) << 24);
+        }
+        *reinterpret_cast<uint32_t*>(cr + c) = word;
+      }
+    }
+    for (int64_t c = cols + lane; c < kpad; c += 64) cr[c] = 0;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = vn[i];
+  }
+}
+
 // General rows (any cols / stride): re-reads the row from cache for each pass.
 __global__ __launch_bounds__(kThreads) void layernorm_quant_kernel(
     const float* __restrict__ x, int64_t rows, int64_t cols, int64_t ldx,
@@ -427,8 +540,9 @@ int qvit_layernorm_quant_i8(const float* x, int64_t rows, int64_t cols, int64_t 
                             const float* gamma, const float* beta, float eps, int qtype,
                             const float* d_quant, const float* q_m, const float* t_quant,
                             int levels, int8_t* codes, int64_t ldc, int64_t kpad,
-                            hipStream_t stream) {
+                            const void* code_table, hipStream_t stream) {
   if (!x || !codes) return QVIT_ENULL;
+  if (code_table && (((uintptr_t)code_table) & 15)) return QVIT_EALIGN;
   if (!qtype_ok(qtype) || !qptrs_ok(qtype, d_quant, q_m, levels)) return QVIT_EINVAL;
   if (rows < 0 || cols <= 0 || ldx < cols || kpad < cols || ldc < kpad) return QVIT_EINVAL;
   if (((ldc & 3) != 0) || (((uintptr_t)codes) & 3)) return QVIT_EALIGN;
@@ -437,6 +551,26 @@ int qvit_layernorm_quant_i8(const float* x, int64_t rows, int64_t cols, int64_t 
                    (!gamma || (((uintptr_t)gamma) & 15) == 0) && (!beta || (((uintptr_t)beta) & 15) == 0);
   const int nv = (int)((cols + 255) / 256);
   const dim3 grid((unsigned)((rows + 3) / 4));
+  if (reg && nv <= 4) {  // persistent: <= 8 workgroups per CU, the table read once per workgroup
+    static const int cus = [] {
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+        n = 256;
+      return n;
+    }();
+    const int64_t pg = std::min<int64_t>((rows + 3) / 4, 8 * (int64_t)cus);
+    const int8_t* tab = reinterpret_cast<const int8_t*>(code_table);
+#define QVIT_LN_P(NV)                                                                                          \
+  hipLaunchKernelGGL(layernorm_quant_persist_kernel<NV>, dim3((unsigned)pg), dim3(kThreads), 0, stream, x, rows, \
+                     cols, ldx, gamma, beta, eps, qtype, d_quant, q_m, t_quant, levels, codes, ldc, kpad, tab)
+    if (nv <= 1) QVIT_LN_P(1);
+    else if (nv <= 2) QVIT_LN_P(2);
+    else if (nv <= 3) QVIT_LN_P(3);
+    else QVIT_LN_P(4);
+#undef QVIT_LN_P
+    return qvit_hip_status(hipGetLastError());
+  }
 #define QVIT_LN_REG(NV)                                                                                   \
   hipLaunchKernelGGL(layernorm_quant_reg_kernel<NV>, grid, dim3(kThreads), 0, stream, x, rows, cols, ldx, \
                      gamma, beta, eps, qtype, d_quant, q_m, t_quant, levels, codes, ldc, kpad)

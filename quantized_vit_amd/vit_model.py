@@ -225,7 +225,8 @@ class Block(nn.Module):
         p_qkv = a.qkv.quant_plan()
         codes = torch.empty((M, p_qkv.kpad), dtype=torch.int8, device=x.device)
         _lib.layernorm_quant_i8(x2, self.norm1.weight, self.norm1.bias, self.norm1.eps, p_qkv.qtype, p_qkv.d_act,
-                                p_qkv.qm_act, p_qkv.t_act, 0, codes, p_qkv.kpad)
+                                p_qkv.qm_act, p_qkv.t_act, 0, codes, p_qkv.kpad,
+                                code_table=epilogue_table(p_qkv, _lib.EPI_I8))
         p_proj = a.proj.quant_plan()
         if a.split_ok(p_qkv):
             # qkv as pre-scaled fp16 hi/lo head planes, then attention + proj's activation quantizer
@@ -263,7 +264,8 @@ class Block(nn.Module):
         p_fc1 = m.fc1.quant_plan()
         codes = torch.empty((M, p_fc1.kpad), dtype=torch.int8, device=x.device)
         _lib.layernorm_quant_i8(x2, self.norm2.weight, self.norm2.bias, self.norm2.eps, p_fc1.qtype, p_fc1.d_act,
-                                p_fc1.qm_act, p_fc1.t_act, 0, codes, p_fc1.kpad)
+                                p_fc1.qm_act, p_fc1.t_act, 0, codes, p_fc1.kpad,
+                                code_table=epilogue_table(p_fc1, _lib.EPI_I8))
         p_fc2 = m.fc2.quant_plan()
         hid = torch.empty((M, p_fc2.kpad), dtype=torch.int8, device=x.device)
         if p_fc2.kpad != p_fc1.n:

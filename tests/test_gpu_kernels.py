@@ -293,3 +293,36 @@ def test_layernorm_quant_vs_oracle(dev, cols):
     assert diff.max() <= 1
     assert (diff > 0).float().mean() <= 5e-4
     assert (got[:, cols:] == 0).all()
+
+
+@pytest.mark.parametrize("cols,rows", [(768, 20000), (192, 40000), (1000, 3000), (768, 7)])
+@pytest.mark.parametrize("qt,t", [(O.LINEAR, 1.0), (O.NONLINEAR, 1.0), (O.NONLINEAR, 0.8)])
+def test_layernorm_quant_code_table_equals_direct(dev, cols, rows, qt, t):
+    """The persistent LayerNorm kernel quantizing through the code table writes exactly the codes of the
+    per-element quantizer (several rows per wave: rows > 8 x 4 x CUs for the larger cases)."""
+    from quantized_vit_amd.quant_layers import epilogue_table_geometry, saturation_level
+    g = torch.Generator().manual_seed(cols + rows)
+    x = (torch.randn(rows, cols, generator=g) * 2 + 0.3).to(dev)
+    gamma = (torch.rand(cols, generator=g) + 0.5).to(dev)
+    beta = (torch.randn(cols, generator=g) * 0.1).to(dev)
+    qm = 3.0
+    d = qm / 127 if qt == O.LINEAR else qm ** t / 127
+    qtc = _lib.QT_LINEAR if qt == O.LINEAR else _lib.QT_NONLINEAR
+    tt = _p(t, dev) if qt == O.NONLINEAR else None
+    geo = epilogue_table_geometry(qtc, d, qm, t, saturation_level(qtc, d, qm, t), False)
+    table = _lib.epi_table_build(_lib.EPI_I8, qtc, _p(d, dev), _p(qm, dev), tt, 0, *geo, dev)
+    assert int(table[12:16].view(torch.int32).item()) == 1
+    kpad = _round_up(cols, 128)
+    outs = []
+    for tab in (None, table):
+        out = torch.full((rows, kpad), 77, dtype=torch.int8, device=dev)
+        _lib.layernorm_quant_i8(x, gamma, beta, 1e-6, qtc, _p(d, dev), _p(qm, dev), tt, 0, out, kpad,
+                                code_table=tab)
+        torch.cuda.synchronize()
+        outs.append(out.cpu())
+    assert torch.equal(outs[0], outs[1])
+    assert (outs[1][:, cols:] == 0).all()
+    ref = O.quant_codes(F.layer_norm(x[:50].cpu(), (cols,), gamma.cpu(), beta.cpu(), 1e-6), qt, d, qm,
+                        t if qt == O.NONLINEAR else None)
+    diff = (outs[1][:50, :cols].float() - ref).abs()
+    assert diff.max() <= 1 and (diff > 0).float().mean() <= 5e-4
