@@ -162,7 +162,7 @@ int qvit_layernorm_quant_i8(const float* x, int64_t rows, int64_t cols, int64_t 
 
 /*
  * Quantized contraction C = epilogue(A_codes @ W_codes^T).
- *   A      : int8 codes [M][lda], K valid columns; K % QVIT_TILE_K == 0, lda % 16 == 0,
+ *   A      : int8 codes [M][lda], K valid columns; K % QVIT_TILE_K == 0 (and K <= 65536 for QVIT_W4), lda % 16 == 0,
  *            A 16-byte aligned, columns past the true in-features must be 0 (the quantizers
  *            above write them so).
  *   Wp     : packed weights from qvit_pack_weight (wfmt, npad rows, kpad == K).

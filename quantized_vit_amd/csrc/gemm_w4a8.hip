@@ -66,14 +66,12 @@ struct Geo {
   static constexpr int TABLE_MAX_NB = (EPI_BYTES - 16) / 8;
 };
 
-QVIT_DEV uint32_t sext4_lo(uint32_t p) {
-  const uint32_t x = p & 0x0F0F0F0Fu;
-  return ((x ^ 0x08080808u) + 0x78787878u) ^ 0x80808080u;
-}
-QVIT_DEV uint32_t sext4_hi(uint32_t p) {
-  const uint32_t x = (p >> 4) & 0x0F0F0F0Fu;
-  return ((x ^ 0x08080808u) + 0x78787878u) ^ 0x80808080u;
-}
+// int4 weights as int8 MFMA operands scaled by 16: a nibble moved to the high half of its byte reads as
+// the signed byte 16 w exactly (w in [-8, 7]), so the unpack is a mask (high nibbles) or a shift and a
+// mask (low nibbles). The accumulators then hold 16 acc (|16 w a| <= 16256: no overflow for K <= 65536)
+// and are shifted back exactly before the epilogue.
+QVIT_DEV uint32_t nib16_lo(uint32_t p) { return (p << 4) & 0xF0F0F0F0u; }
+QVIT_DEV uint32_t nib16_hi(uint32_t p) { return p & 0xF0F0F0F0u; }
 
 // Lane id from a volatile asm: values derived from it are recomputed where used instead of being
 // hoisted out of the tile loop (which would keep them live across the register-bound main loop).
@@ -359,7 +357,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
       v4i wf;
       if (WFMT == QVIT_W4) {
         const uint2 p = f.w4[r];
-        wf = v4i{(int)sext4_lo(p.x), (int)sext4_hi(p.x), (int)sext4_lo(p.y), (int)sext4_hi(p.y)};
+        wf = v4i{(int)nib16_lo(p.x), (int)nib16_hi(p.x), (int)nib16_lo(p.y), (int)nib16_hi(p.y)};
       } else {
         wf = f.w8[r];
       }
@@ -443,6 +441,14 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     step_core(fb, fa, 0, false);
     QVIT_STAMP(3);
 
+    if (WFMT == QVIT_W4) {  // 16 acc -> acc (exact arithmetic shift)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int sr = 0; sr < 8; ++sr)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[r][sr][j] >>= 4;
+    }
 #if defined(QVIT_GEMM_ABL)
     if (QVIT_GEMM_ABL == 6) {  // diagnostic: no epilogue (accumulators folded into one store per lane)
       int x = 0;
@@ -767,6 +773,7 @@ extern "C" int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda, con
   if (wfmt != QVIT_W4 && wfmt != QVIT_W8) return QVIT_EINVAL;
   if (M < 0 || K <= 0 || K % KTILE || lda < K || N <= 0 || npad < N || npad % BN) return QVIT_EINVAL;
   if (M > INT32_MAX / 2 || npad > INT32_MAX / 2 || K > (1 << 24)) return QVIT_EINVAL;
+  if (wfmt == QVIT_W4 && K > 65536) return QVIT_EINVAL;  // 16x-scaled int32 accumulation bound
   if ((lda % 16) || (((uintptr_t)A) & 15) || (((uintptr_t)Wp) & 15)) return QVIT_EALIGN;
   if (epilogue < QVIT_EPI_F32 || epilogue > QVIT_EPI_I32) return QVIT_EINVAL;
   const bool i8out = epilogue == QVIT_EPI_I8 || epilogue == QVIT_EPI_I8_GELU;
@@ -809,6 +816,7 @@ extern "C" int qvit_gemm_qkv_split(const int8_t* A, int64_t M, int64_t K, int64_
   if (M < 0 || K <= 0 || K % KTILE || lda < K || N <= 0 || N % 64 || npad < N || npad % BN) return QVIT_EINVAL;
   if (M > INT32_MAX / 2 || npad > INT32_MAX / 2 || K > (1 << 24)) return QVIT_EINVAL;
   if (seq <= 0 || seq > (1 << 20) || M % seq || !(in_scale > 0.f)) return QVIT_EINVAL;
+  if (wfmt == QVIT_W4 && K > 65536) return QVIT_EINVAL;
   if ((lda % 16) || (((uintptr_t)A) & 15) || (((uintptr_t)Wp) & 15)) return QVIT_EALIGN;
   if ((((uintptr_t)qkv_hi) & 15) || (((uintptr_t)qkv_lo) & 15)) return QVIT_EALIGN;
   if (bias && (((uintptr_t)bias) & 15)) return QVIT_EALIGN;
