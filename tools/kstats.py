@@ -68,9 +68,14 @@ def pmc(fetch_dir, write_dir, rnd):
     }
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     os.makedirs(os.path.join(root, "profiles"), exist_ok=True)
-    for name in (f"fc1_traffic_{rnd}.json", "fc1_traffic.json"):
-        with open(os.path.join(root, "profiles", name), "w") as fh:
-            json.dump(out, fh, indent=1)
+    dirs = [os.path.join(root, "profiles")]
+    if os.environ.get("PMC_OUT"):   # on the GPU box only gpurun_out/ travels back
+        dirs.append(os.environ["PMC_OUT"])
+    for d in dirs:
+        os.makedirs(d, exist_ok=True)
+        for name in (f"fc1_traffic_{rnd}.json", "fc1_traffic.json"):
+            with open(os.path.join(d, name), "w") as fh:
+                json.dump(out, fh, indent=1)
     print(json.dumps(out, indent=1))
 
 
