@@ -92,6 +92,32 @@ QVIT_DEV float xsum(float v) {
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
+// Diagnostic build only (-DQVIT_ATT_STAMPS, tools/attn_bench.py --stamps): per-phase s_memtime sums
+// (0 block wait + DMA issue, 1 scores, 2 softmax, 3 PV, 4 epilogue, 5 query-block reads).
+#ifdef QVIT_ATT_STAMPS
+__device__ unsigned long long qvit_att_stamp_sums[8];
+struct Stamps {
+  unsigned long long a[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long prev = __builtin_amdgcn_s_memtime();
+  QVIT_DEV void mark(int i) {
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    a[i] += t - prev;
+    prev = t;
+  }
+  QVIT_DEV void flush() {
+    if ((threadIdx.x & 63) == 0) {
+      for (int i = 0; i < 6; ++i) atomicAdd(&qvit_att_stamp_sums[i], a[i]);
+      atomicAdd(&qvit_att_stamp_sums[7], 1ull);
+    }
+  }
+};
+#else
+struct Stamps {
+  QVIT_DEV void mark(int) {}
+  QVIT_DEV void flush() {}
+};
+#endif
+
 // Online-softmax update of one key block (KB keys in the LDS images at st) for a wave's first NT query
 // tiles, in three phases that keep the live fragments small (2 waves per SIMD leave 256 registers):
 //   1. S^T = K . Q^T for every tile (K fragments live only here);
@@ -103,7 +129,7 @@ QVIT_DEV float xsum(float v) {
 // MASK: the block holds keys >= N (the last block only).
 QVIT_DEV void attend(int nt, bool mask, const int8_t* st, const h8 (&qh)[QTW][2], const h8 (&ql)[QTW][2], float (&m)[QTW],
                      float (&l)[QTW], f4 (&o)[QTW][4], const int (&koffs)[2][2], const int (&voffs)[4], int kbase,
-                     int N, float sl2) {
+                     int N, float sl2, Stamps& sp) {
 #if defined(QVIT_ATT_ABL) && QVIT_ATT_ABL == 1
   return;  // diagnostic: operand streaming only
 #endif
@@ -128,6 +154,7 @@ QVIT_DEV void attend(int nt, bool mask, const int8_t* st, const h8 (&qh)[QTW][2]
         for (int c = 0; c < 2; ++c) s[i][kt] = mfma3(kh[kt][c], kl[kt][c], qh[i][c], ql[i][c], s[i][kt]);
       }
   }
+  sp.mark(1);
   h8 ph[NT], pl[NT];
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
@@ -167,6 +194,7 @@ QVIT_DEV void attend(int nt, bool mask, const int8_t* st, const h8 (&qh)[QTW][2]
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[i][dt] = o[i][dt] * alpha;
   }
+  sp.mark(2);
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) {
     const h8 vh = join(tr_read(st + 2 * IMG, voffs[dt]), tr_read(st + 2 * IMG, voffs[dt] + 16 * 128));
@@ -175,13 +203,14 @@ QVIT_DEV void attend(int nt, bool mask, const int8_t* st, const h8 (&qh)[QTW][2]
     for (int i = 0; i < NT - 1; ++i) o[i][dt] = mfma3(vh, vl, ph[i], pl[i], o[i][dt]);
     if (nt == NT) o[NT - 1][dt] = mfma3(vh, vl, ph[NT - 1], pl[NT - 1], o[NT - 1][dt]);
   }
+  sp.mark(3);
 }
 
 // nt >= 3 (the fused shapes) or the general case: tiles past nt are skipped (wave-uniform branches).
 QVIT_DEV void attend_n(int nt, bool mask, const int8_t* st, const h8 (&qh)[QTW][2], const h8 (&ql)[QTW][2],
                        float (&m)[QTW], float (&l)[QTW], f4 (&o)[QTW][4], const int (&koffs)[2][2],
-                       const int (&voffs)[4], int kbase, int N, float sl2) {
-  attend(nt, mask, st, qh, ql, m, l, o, koffs, voffs, kbase, N, sl2);
+                       const int (&voffs)[4], int kbase, int N, float sl2, Stamps& sp) {
+  attend(nt, mask, st, qh, ql, m, l, o, koffs, voffs, kbase, N, sl2, sp);
 }
 
 // The int8 epilogue's code table in LDS (qvit_epi_table_build with QVIT_EPI_I8 semantics), if any.
@@ -384,8 +413,9 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const float* __restrict__ 
   __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
     if (kb + 1 < nkb) load_block(kb + 1);
+    Stamps sp;
     attend_n(nt, (kb + 1) * KB > N, smem + (kb & 1) * STAGE, qh, ql, m, l, o, koffs, voffs, kb * KB + 4 * g, N,
-             sl2);
+             sl2, sp);
     if (kb + 1 < nkb) {
       __syncthreads();  // every wave is done with buffer (kb + 1) & 1 (used by block kb - 1)
       store_block((kb + 1) & 1);
@@ -531,6 +561,7 @@ __global__ __launch_bounds__(256, 2) void attn_split_kernel(const _Float16* __re
   fragment_offsets(koffs, voffs);
   const float sl2 = scale * LOG2E / (in_scale * in_scale);
 
+  Stamps sp;
   for (int p = 0; p < 3 && p < total; ++p) issue(p);
   int p = 0;
   for (int j = 0; j < my_units; ++j) {
@@ -544,7 +575,9 @@ __global__ __launch_bounds__(256, 2) void attn_split_kernel(const _Float16* __re
 #pragma unroll
     for (int i = 0; i < QTW; ++i) {
       if (i < nqb) {
+        sp.mark(4);
         sync(p);
+        sp.mark(0);
         const int8_t* st = smem + (p & (SRING - 1)) * STAGE;
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
@@ -567,16 +600,20 @@ __global__ __launch_bounds__(256, 2) void attn_split_kernel(const _Float16* __re
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) o[i][dt] = f4{0.f, 0.f, 0.f, 0.f};
     }
+    sp.mark(5);
     for (int kb = 0; kb < nkb; ++kb, ++p) {
       sync(p);
+      sp.mark(0);
       attend_n(nt, (kb + 1) * KB > N, smem + (p & (SRING - 1)) * STAGE, qh, ql, m, l, o, koffs, voffs,
-               kb * KB + 4 * g, N, sl2);
+               kb * KB + 4 * g, N, sl2, sp);
     }
     bool tv[QTW];
 #pragma unroll
     for (int i = 0; i < QTW; ++i) tv[i] = i < nt;
     attend_store<OUT>(tv, l, o, wr, q0, N, b, h, in_scale, out, ldo, qp, tb, st16);
   }
+  sp.mark(4);
+  sp.flush();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -659,3 +696,13 @@ extern "C" int qvit_attention_split(const void* qkv_hi, const void* qkv_lo, int6
                        reinterpret_cast<const int8_t*>(epi_table));
   return qvit_hip_status(hipGetLastError());
 }
+
+#ifdef QVIT_ATT_STAMPS
+extern "C" int qvit_att_stamps(unsigned long long* host8, int reset) {
+  if (reset) {
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    return qvit_hip_status(hipMemcpyToSymbol(HIP_SYMBOL(qvit_att_stamp_sums), z, sizeof(z)));
+  }
+  return qvit_hip_status(hipMemcpyFromSymbol(host8, HIP_SYMBOL(qvit_att_stamp_sums), 8 * sizeof(unsigned long long)));
+}
+#endif

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--lib", default="", help="load this library build instead (diagnostic variants)")
     ap.add_argument("--split-only", action="store_true")
+    ap.add_argument("--stamps", action="store_true", help="with a -DQVIT_ATT_STAMPS --lib: phase cycles")
     a = ap.parse_args()
     if a.lib:
         _lib.load(a.lib)
@@ -50,12 +51,32 @@ def main():
 
     hi = qkv.half().reshape(-1)
     lo = (qkv - qkv.half().float()).half().reshape(-1)
+    from quantized_vit_amd.quant_layers import epilogue_table_geometry, saturation_level
+    geo = epilogue_table_geometry(_lib.QT_NONLINEAR, 2.0 / 127, 2.0, 1.0,
+                                  saturation_level(_lib.QT_NONLINEAR, 2.0 / 127, 2.0, 1.0), False)
+    table = _lib.epi_table_build(_lib.EPI_I8, _lib.QT_NONLINEAR, d, qm, t, 0, *geo, dev)   # as the model does
     sp = timeit(lambda: _lib.attention_split(hi, lo, B, N, H, 64, 0.125, codes, _lib.ATT_I8, 1.0, _lib.QT_NONLINEAR,
-                                             d, qm, t), a.iters)
+                                             d, qm, t, epi_table=table), a.iters)
     spf = timeit(lambda: _lib.attention_split(hi, lo, B, N, H, 64, 0.125, out), a.iters)
     flops = 4.0 * B * H * N * N * 64
     print(f"{'split i8':20s} {sp*1e3:9.1f} us  {flops/sp/1e9:8.1f} TFLOP/s (fp32-equivalent)", flush=True)
     print(f"{'split f32':20s} {spf*1e3:9.1f} us  {flops/spf/1e9:8.1f} TFLOP/s (fp32-equivalent)", flush=True)
+    if a.stamps:
+        import ctypes
+        lib = _lib.load()
+        lib.qvit_att_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        buf = (ctypes.c_ulonglong * 8)()
+        torch.cuda.synchronize()
+        assert lib.qvit_att_stamps(buf, 1) == 0
+        _lib.attention_split(hi, lo, B, N, H, 64, 0.125, codes, _lib.ATT_I8, 1.0, _lib.QT_NONLINEAR, d, qm, t,
+                             epi_table=table)
+        torch.cuda.synchronize()
+        assert lib.qvit_att_stamps(buf, 0) == 0
+        waves = max(buf[7], 1)
+        per = [buf[i] / waves for i in range(6)]
+        names = ["wait+issue", "scores", "softmax", "PV", "epilogue", "q-reads"]
+        tot = sum(per)
+        print("per wave: " + "  ".join(f"{n} {v:8.0f} ({100*v/tot:4.1f}%)" for n, v in zip(names, per)))
     if a.split_only:
         return
     f32 = timeit(lambda: _lib.attention(qkv, B, N, H, 64, 0.125, out), a.iters)
