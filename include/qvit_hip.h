@@ -274,6 +274,22 @@ int qvit_attention_split(const void* qkv_hi, const void* qkv_lo, int64_t B, int6
                          int64_t ldo, int out_qtype, const float* out_d, const float* out_qm,
                          const float* out_t, int out_levels, const void* epi_table, hipStream_t stream);
 
+/*
+ * Fused qkv projection + attention core (vit_model.py:130-152) for the fused block: the qkv
+ * QuantizeLinear (qvit_gemm_qkv_split semantics: d_act d_wt acc + bias, scaled by in_scale, split to
+ * fp16 hi/lo) and qvit_attention_split in one kernel, q/k/v never written to HBM.
+ *   A    : activation codes [B*N][lda] (K valid columns, K % 256 == 0, K <= 65536), N <= 208 tokens, H*64 <= 768;
+ *   Wp   : the qkv layer's packed int4 weights (qvit_pack_weight, wfmt QVIT_W4, npad rows), bias [npad];
+ *   out  : as qvit_attention_split (QVIT_ATT_F32 / QVIT_ATT_I8 + optional code table epi_table).
+ * The dims of each q.k sum are added in a different order than in qvit_attention_split (fp32-level
+ * differences only).
+ */
+int qvit_qkv_attention(const int8_t* A, int64_t B, int64_t N, int64_t K, int64_t lda, const void* Wp,
+                       int wfmt, int64_t npad, const float* d_act, const float* d_wt, const float* bias,
+                       int64_t H, int64_t head_dim, float scale, float in_scale, int out_mode, void* out,
+                       int64_t ldo, int out_qtype, const float* out_d, const float* out_qm,
+                       const float* out_t, int out_levels, const void* epi_table, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

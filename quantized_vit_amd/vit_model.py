@@ -228,6 +228,18 @@ class Block(nn.Module):
                                 p_qkv.qm_act, p_qkv.t_act, 0, codes, p_qkv.kpad,
                                 code_table=epilogue_table(p_qkv, _lib.EPI_I8))
         p_proj = a.proj.quant_plan()
+        if (a.split_ok(p_qkv) and N <= _lib.QKV_ATT_MAX_N and p_qkv.wfmt == _lib.W4 and p_qkv.kpad <= 65536
+                and p_qkv.kpad % 256 == 0 and a.num_heads * 64 <= _lib.QKV_ATT_MAX_C):
+            # qkv projection + attention + proj's activation quantizer in one kernel (q/k/v stay on chip)
+            out = torch.empty((M, p_proj.kpad), dtype=torch.int8, device=x.device)
+            if p_proj.kpad != a.num_heads * 64:
+                out[:, a.num_heads * 64:].zero_()
+            _lib.qkv_attention(codes, B, N, p_qkv.kpad, p_qkv.packed, p_qkv.npad, p_qkv.d_act, p_qkv.d_wt,
+                               p_qkv.bias_pad, a.num_heads, a.scale, out, _lib.ATT_I8, attention_in_scale(p_qkv),
+                               p_proj.qtype, p_proj.d_act, p_proj.qm_act, p_proj.t_act,
+                               epi_table=epilogue_table(p_proj, _lib.EPI_I8))
+            a.proj.gemm_codes(out, p_proj, _lib.EPI_F32_RESID, out=x2)
+            return self._mlp_fused_(x, x2, M)
         if a.split_ok(p_qkv):
             # qkv as pre-scaled fp16 hi/lo head planes, then attention + proj's activation quantizer
             in_scale = attention_in_scale(p_qkv)

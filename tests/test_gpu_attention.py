@@ -237,3 +237,81 @@ def test_attention_split_code_table_equals_direct(dev, qt, t, ldo):
     assert torch.equal(outs[0][:, :H * 64], ref) and torch.equal(outs[1][:, :H * 64], ref)
     assert (outs[1][:, H * 64:] == 0).all()
     assert len(torch.unique(ref)) > 100
+
+
+# ---- fused qkv projection + attention (qvit_qkv_attention) -------------------------------------------
+def _fused_case(dev, B, N, H, seed, K=768):
+    from test_gpu_kernels import act_buffer, pack_codes
+    g = torch.Generator().manual_seed(seed)
+    C = 64 * H
+    a = torch.randint(-60, 61, (B * N, K), generator=g)
+    w = torch.randint(-7, 8, (3 * C, K), generator=g)
+    bias = torch.randn(3 * C, generator=g) * 0.3
+    packed, npad, kpad = pack_codes(w, _lib.W4, dev)
+    bias_pad = _lib.pad_bias(bias.to(dev), 3 * C, npad, dev)
+    return act_buffer(a, kpad, dev), packed, npad, kpad, bias_pad, _p(0.004, dev), _p(0.003, dev)
+
+
+def _split_path(dev, B, N, H, A, packed, npad, kpad, bias_pad, da, dw, s, out, mode, **kw):
+    C = 64 * H
+    hi = torch.empty(B * N * 3 * C, dtype=torch.float16, device=dev)
+    lo = torch.empty_like(hi)
+    _lib.gemm_qkv_split(A, B * N, kpad, packed, _lib.W4, 3 * C, npad, da, dw, bias_pad, N, s, hi, lo)
+    _lib.attention_split(hi, lo, B, N, H, 64, 0.125, out, mode, s, **kw)
+    torch.cuda.synchronize()
+    return out.cpu()
+
+
+@pytest.mark.parametrize("B,N,H", [(3, 197, 12), (2, 50, 4), (1, 208, 2), (5, 1, 3), (2, 17, 12), (9, 100, 1)])
+def test_qkv_attention_fused_f32_vs_split_path(dev, B, N, H):
+    A, packed, npad, kpad, bias_pad, da, dw = _fused_case(dev, B, N, H, seed=B * 1000 + N + H)
+    ref = _split_path(dev, B, N, H, A, packed, npad, kpad, bias_pad, da, dw, 2.0 ** -2,
+                      torch.full((B * N, 64 * H), float("nan"), device=dev), _lib.ATT_F32)
+    out = torch.full((B * N, 64 * H), float("nan"), device=dev)
+    _lib.qkv_attention(A, B, N, kpad, packed, npad, da, dw, bias_pad, H, 0.125, out, _lib.ATT_F32, 2.0 ** -2)
+    torch.cuda.synchronize()
+    got = out.cpu()
+    assert torch.isfinite(got).all()
+    err = (got.double() - ref.double()).abs().max().item()
+    assert err <= 2e-6 * ref.abs().max().item(), err
+
+
+@pytest.mark.parametrize("B,N,H", [(4, 197, 12), (3, 64, 6)])
+def test_qkv_attention_fused_int8_codes(dev, B, N, H):
+    from quantized_vit_amd.quant_layers import epilogue_table_geometry, saturation_level
+    A, packed, npad, kpad, bias_pad, da, dw = _fused_case(dev, B, N, H, seed=7 + N)
+    qm, t = 0.5, 0.9
+    d = qm ** t / 127
+    kw = dict(out_qtype=_lib.QT_NONLINEAR, out_d=_p(d, dev), out_qm=_p(qm, dev), out_t=_p(t, dev))
+    geo = epilogue_table_geometry(_lib.QT_NONLINEAR, d, qm, t, saturation_level(_lib.QT_NONLINEAR, d, qm, t), False)
+    table = _lib.epi_table_build(_lib.EPI_I8, _lib.QT_NONLINEAR, kw["out_d"], kw["out_qm"], kw["out_t"], 0, *geo,
+                                 dev)
+    ref = _split_path(dev, B, N, H, A, packed, npad, kpad, bias_pad, da, dw, 1.0,
+                      torch.zeros((B * N, 64 * H), dtype=torch.int8, device=dev), _lib.ATT_I8, epi_table=table, **kw)
+    out = torch.full((B * N, 64 * H), 99, dtype=torch.int8, device=dev)
+    _lib.qkv_attention(A, B, N, kpad, packed, npad, da, dw, bias_pad, H, 0.125, out, _lib.ATT_I8, 1.0,
+                       epi_table=table, **kw)
+    torch.cuda.synchronize()
+    diff = (out.cpu().to(torch.int32) - ref.to(torch.int32)).abs()
+    assert diff.max().item() <= 1
+    assert (diff > 0).float().mean().item() <= 1e-3
+    assert len(torch.unique(ref)) > 60
+
+
+def test_qkv_attention_argument_validation(dev):
+    lib = _lib.load()
+    s = torch.cuda.current_stream().cuda_stream
+    buf = torch.zeros(1 << 16, dtype=torch.int8, device=dev)
+    p = buf.data_ptr()
+    one = _p(1.0, dev).data_ptr()
+    args = lambda **o: [o.get("A", p), o.get("B", 1), o.get("N", 10), o.get("K", 256), o.get("lda", 256), p,
+                        o.get("wfmt", 4), o.get("npad", 256), one, one, None, o.get("H", 1), o.get("hd", 64), 0.125,
+                        1.0, 0, p, 64, 0, None, None, None, 0, None, s]
+    assert lib.qvit_qkv_attention(*args()) == 0
+    assert lib.qvit_qkv_attention(*args(N=209)) == -1        # N > 208
+    assert lib.qvit_qkv_attention(*args(wfmt=8)) == -1       # int4 weights only
+    assert lib.qvit_qkv_attention(*args(K=128, lda=256)) == -1   # K % 256
+    assert lib.qvit_qkv_attention(*args(hd=32)) == -1
+    assert lib.qvit_qkv_attention(*args(A=None)) == -3
+    assert lib.qvit_qkv_attention(*args(A=p + 4)) == -2
+    torch.cuda.synchronize()

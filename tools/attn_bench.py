@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--lib", default="", help="load this library build instead (diagnostic variants)")
     ap.add_argument("--split-only", action="store_true")
+    ap.add_argument("--fused", action="store_true", help="also time qvit_qkv_attention (+ the qkv split GEMM)")
     ap.add_argument("--stamps", action="store_true", help="with a -DQVIT_ATT_STAMPS --lib: phase cycles")
     a = ap.parse_args()
     if a.lib:
@@ -65,18 +66,53 @@ def main():
         import ctypes
         lib = _lib.load()
         lib.qvit_att_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
-        buf = (ctypes.c_ulonglong * 8)()
+        buf = (ctypes.c_ulonglong * 16)()
         torch.cuda.synchronize()
         assert lib.qvit_att_stamps(buf, 1) == 0
         _lib.attention_split(hi, lo, B, N, H, 64, 0.125, codes, _lib.ATT_I8, 1.0, _lib.QT_NONLINEAR, d, qm, t,
                              epi_table=table)
         torch.cuda.synchronize()
         assert lib.qvit_att_stamps(buf, 0) == 0
-        waves = max(buf[7], 1)
+        waves = max(buf[15], 1)
         per = [buf[i] / waves for i in range(6)]
         names = ["wait+issue", "scores", "softmax", "PV", "epilogue", "q-reads"]
         tot = sum(per)
         print("per wave: " + "  ".join(f"{n} {v:8.0f} ({100*v/tot:4.1f}%)" for n, v in zip(names, per)))
+    if a.fused:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from test_gpu_kernels import act_buffer, pack_codes
+        g = torch.Generator().manual_seed(1)
+        C = 64 * H
+        acodes = torch.randint(-60, 61, (B * N, 768), generator=g)
+        w = torch.randint(-7, 8, (3 * C, 768), generator=g)
+        packed, npad, kpad = pack_codes(w, _lib.W4, dev)
+        bias_pad = _lib.pad_bias((torch.randn(3 * C, generator=g) * 0.3).to(dev), 3 * C, npad, dev)
+        A = act_buffer(acodes, kpad, dev)
+        da, dw = torch.tensor([0.004], device=dev), torch.tensor([0.003], device=dev)
+        fz = lambda: _lib.qkv_attention(A, B, N, kpad, packed, npad, da, dw, bias_pad, H, 0.125, codes, _lib.ATT_I8,
+                                        1.0, _lib.QT_NONLINEAR, d, qm, t, epi_table=table)
+        ms = timeit(fz, a.iters)
+        print(f"{'fused qkv+attn i8':20s} {ms*1e3:9.1f} us", flush=True)
+        hi2 = torch.empty(B * N * 3 * C, dtype=torch.float16, device=dev)
+        lo2 = torch.empty_like(hi2)
+        ms2 = timeit(lambda: _lib.gemm_qkv_split(A, B * N, kpad, packed, _lib.W4, 3 * C, npad, da, dw, bias_pad, N, 1.0,
+                                                 hi2, lo2), a.iters)
+        print(f"{'qkv split gemm':20s} {ms2*1e3:9.1f} us", flush=True)
+        if a.stamps:
+            import ctypes
+            lib = _lib.load()
+            lib.qvit_qkv_att_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+            buf = (ctypes.c_ulonglong * 16)()
+            torch.cuda.synchronize()
+            assert lib.qvit_qkv_att_stamps(buf, 1) == 0
+            fz()
+            torch.cuda.synchronize()
+            assert lib.qvit_qkv_att_stamps(buf, 0) == 0
+            waves = max(buf[15], 1)
+            per = [buf[i] / waves for i in range(8)]
+            names = ["-", "proj reads+mfma", "epilogue", "attention", "store", "load issue", "w write(wait)", "barrier"]
+            tot = sum(per)
+            print("fused per wave: " + "  ".join(f"{n} {v:8.0f} ({100*v/tot:4.1f}%)" for n, v in zip(names, per)))
     if a.split_only:
         return
     f32 = timeit(lambda: _lib.attention(qkv, B, N, H, 64, 0.125, out), a.iters)
