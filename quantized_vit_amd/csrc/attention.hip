@@ -222,7 +222,7 @@ __global__ __launch_bounds__(256, 2) void attn_split_kernel(const _Float16* __re
         int8_t* tl = smem + SRING * STAGE;
         for (int k = tid; k < (16 + 8 * hd.nb + 15) / 16; k += 256)
           reinterpret_cast<uint4*>(tl)[k] = reinterpret_cast<const uint4*>(epi_table)[k];
-        tb = EpiLds{tl + sizeof(EpiTableHdr), hd.c0, hd.inv_w, (float)(hd.nb - 1)};
+        tb = EpiLds{tl + sizeof(EpiTableHdr), hd.c0, hd.inv_w, epi_top(hd.nb)};
       }
     }
   }

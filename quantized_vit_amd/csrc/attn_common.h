@@ -184,7 +184,7 @@ QVIT_DEV void attend(int nt, bool mask, const int8_t* st, const h8 (&qh)[T][2], 
 // The int8 epilogue's code table in LDS (qvit_epi_table_build with QVIT_EPI_I8 semantics), if any.
 struct EpiLds {
   const int8_t* ent;  // entries (header excluded), nullptr -> per-element quantizer
-  float c0, inv_w, nbm1;
+  float c0, inv_w, top;  // table geometry (EpiTableHdr, epi_top)
 };
 
 // 4x4 transpose between the lane groups g (lanes 16g..16g+15) and the 4 registers: afterwards lane g
@@ -231,7 +231,7 @@ QVIT_DEV void attend_store(const bool (&tv)[T], const float (&l)[T], const f4 (&
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           v[dt][j] = o[i][dt][j] * inv;
-          e[dt][j] = *reinterpret_cast<const uint2*>(tb.ent + (epi_bucket(v[dt][j], tb.c0, tb.inv_w, tb.nbm1) << 3));
+          e[dt][j] = *epi_entry(tb.ent, v[dt][j], tb.c0, tb.inv_w, tb.top);
         }
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {

@@ -156,8 +156,10 @@ __global__ void epi_table_kernel(int gelu, int out_qtype, const float* out_d, co
   EpiTableHdr* hdr = reinterpret_cast<EpiTableHdr*>(table);
   EpiTableEnt* ent = reinterpret_cast<EpiTableEnt*>(table + sizeof(EpiTableHdr));
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const float C = c0 + 8388608.f;  // epi_bucket_bits
+  const float top = epi_top(nb);
   if (j == 0) {
-    hdr->c0 = c0;
+    hdr->c0 = C;
     hdr->inv_w = inv_w;
     hdr->nb = nb;
   }
@@ -167,7 +169,7 @@ __global__ void epi_table_kernel(int gelu, int out_qtype, const float* out_d, co
     int lo = fkey(-3.0e38f), hi = fkey(3.0e38f);
     while (lo < hi) {
       const int mid = lo + ((hi - lo) >> 1);
-      if (epi_bucket(funkey(mid), c0, inv_w, (float)(nb - 1)) >= b) hi = mid;
+      if (epi_bucket(funkey(mid), C, inv_w, top) >= b) hi = mid;
       else lo = mid + 1;
     }
     return lo;
@@ -272,12 +274,18 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   const int hi = lo + per + (xcd < rem ? 1 : 0);
   int t = lo + slot;
   if (t >= hi) return;
+#if defined(QVIT_GEMM_STAGGER)
+  if (blockIdx.x >= (gridDim.x >> 1))
+    for (int i = 0; i < QVIT_GEMM_STAGGER; ++i) __builtin_amdgcn_s_sleep(64);
+#endif
 
   // epilogue scalars and the code table are set up before the main loop
+  // W4 accumulators hold 16 acc exactly: the float epilogues fold the 1/16 into alpha, which gives the very
+  // same fp32 results (float(16 acc) = 16 float(acc), and alpha/16 is exact), one shift per element cheaper
   float alpha = 0.f;
-  if (EPI != QVIT_EPI_I32) alpha = (*ep.d_act) * (*ep.d_wt);
+  if (EPI != QVIT_EPI_I32) alpha = (*ep.d_act) * (*ep.d_wt) * (WFMT == QVIT_W4 ? 0.0625f : 1.f);
   bool use_table = false;
-  float t_c0 = 0.f, t_invw = 0.f;
+  float t_c0 = 0.f, t_invw = 0.f, t_top = 0.f;
   int t_nb = 1;
   if (I8OUT && ep.table != nullptr) {
     const EpiTableHdr h = *reinterpret_cast<const EpiTableHdr*>(ep.table);
@@ -285,6 +293,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     t_c0 = h.c0;
     t_invw = h.inv_w;
     t_nb = h.nb;
+    t_top = epi_top(h.nb);
     if (use_table) {  // -> the epilogue region, once per block (made visible by the first stage sync)
       const v4i* src = reinterpret_cast<const v4i*>(ep.table);
       for (int i = tid; i < (16 + 8 * t_nb + 15) / 16; i += G::NT) reinterpret_cast<v4i*>(epi_lds)[i] = src[i];
@@ -373,7 +382,13 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   auto step_core = [&](Frags<WFMT>& cur, Frags<WFMT>& nxt, int next_slot, bool read) __attribute__((always_inline)) {
     if (read) read_frags(next_slot, nxt);
     __builtin_amdgcn_sched_barrier(0);
+#if defined(QVIT_GEMM_PRIO)
+    __builtin_amdgcn_s_setprio(1);
+#endif
     mfma_stage(cur);
+#if defined(QVIT_GEMM_PRIO)
+    __builtin_amdgcn_s_setprio(0);
+#endif
     __builtin_amdgcn_sched_barrier(0);
   };
 
@@ -441,7 +456,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     step_core(fb, fa, 0, false);
     QVIT_STAMP(3);
 
-    if (WFMT == QVIT_W4) {  // 16 acc -> acc (exact arithmetic shift)
+    if (WFMT == QVIT_W4 && EPI == QVIT_EPI_I32) {  // 16 acc -> acc (exact arithmetic shift)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -476,12 +491,12 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
         if (has_bias) b = *reinterpret_cast<const float4*>(bias_l + (nbase - n0) + 4 * r);
         bcol[4 * r] = b.x; bcol[4 * r + 1] = b.y; bcol[4 * r + 2] = b.z; bcol[4 * r + 3] = b.w;
       }
-      const bool c16 = ((ldc & 15) == 0) && ((((uintptr_t)C) & 15) == 0);
+      // 16-B row stores when every row segment is whole and aligned (kernel-uniform); else byte stores
+      const bool fast16 = ((ldc & 15) == 0) && ((((uintptr_t)C) & 15) == 0) && ((N & 15) == 0);
 #pragma unroll
       for (int sr = 0; sr < 8; ++sr) {
         const int m = m0 + 128 * wm + 16 * sr + efr;
         uint32_t wd[4];
-        const float nbm1 = (float)(t_nb - 1);
         // the row's 16 lookups are issued together, then resolved (one LDS latency per row)
         float v[4][4];
         uint2 e[4][4];
@@ -490,7 +505,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             v[r][j] = fmaf(alpha, (float)acc[r][sr][j], bcol[4 * r + j]);
-            e[r][j] = *reinterpret_cast<const uint2*>(tlb + (epi_bucket(v[r][j], t_c0, t_invw, nbm1) << 3));
+            e[r][j] = *epi_entry(tlb, v[r][j], t_c0, t_invw, t_top);
           }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -500,19 +515,13 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
           epi_select_byte<2>(wd[r], v[r][2], __uint_as_float(e[r][2].x), e[r][2].y);
           epi_select_byte<3>(wd[r], v[r][3], __uint_as_float(e[r][3].x), e[r][3].y);
         }
-        if (m < M) {
-          int8_t* dst = reinterpret_cast<int8_t*>(C) + (int64_t)m * ldc + nbase;
-          if (nbase + 16 <= N) {
-            if (c16) {
-              *reinterpret_cast<uint4*>(dst) = make_uint4(wd[0], wd[1], wd[2], wd[3]);
-            } else {
+        int8_t* dst = reinterpret_cast<int8_t*>(C) + (int64_t)m * ldc + nbase;
+        if (fast16) {
+          if (m < M && nbase < N) *reinterpret_cast<uint4*>(dst) = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+        } else if (m < M) {
 #pragma unroll
-              for (int r = 0; r < 4; ++r) reinterpret_cast<uint32_t*>(dst)[r] = wd[r];
-            }
-          } else {
-            for (int q = 0; q < 16; ++q)
-              if (nbase + q < N) dst[q] = (int8_t)((wd[q >> 2] >> (8 * (q & 3))) & 0xff);
-          }
+          for (int q = 0; q < 16; ++q)
+            if (nbase + q < N) dst[q] = (int8_t)((wd[q >> 2] >> (8 * (q & 3))) & 0xff);
         }
       }
     } else if (EPI == QVIT_EPI_F32_RESID) {
@@ -715,14 +724,19 @@ int device_cus() {
 template <int WFMT, int EPI>
 int launch(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int64_t N, int64_t npad,
            void* C, int64_t ldc, const EpiArgs& ep, hipStream_t stream) {
-  using G = Geo<WFMT, 1>;
+#if defined(QVIT_GEMM_WM)
+  constexpr int WMV = (WFMT == QVIT_W4) ? QVIT_GEMM_WM : 1;
+#else
+  constexpr int WMV = 1;
+#endif
+  using G = Geo<WFMT, WMV>;
   const int64_t ntiles = (npad / BN) * ((M + G::BM - 1) / G::BM);
   // resident blocks, a multiple of 8 (one team per XCD), no more than the tiles need
   int64_t grid = (int64_t)device_cus() * G::MIN_BLOCKS / 8 * 8;
   const int64_t need = (ntiles + 7) / 8 * 8;
   if (grid > need) grid = need;
   if (grid < 8) grid = 8;
-  hipLaunchKernelGGL((gemm_kernel<WFMT, EPI, 1>), dim3((unsigned)grid), dim3(G::NT), 0, stream, A, (int)M, (int)K,
+  hipLaunchKernelGGL((gemm_kernel<WFMT, EPI, WMV>), dim3((unsigned)grid), dim3(G::NT), 0, stream, A, (int)M, (int)K,
                      lda, reinterpret_cast<const int8_t*>(Wp), (int)N, (int)npad, C, ldc, ep);
   return qvit_hip_status(hipGetLastError());
 }

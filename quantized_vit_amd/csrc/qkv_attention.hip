@@ -69,7 +69,7 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
       if (hd.valid != 0 && hd.nb >= 1 && 16 + 8 * hd.nb <= TBL) {
         for (int k = tid; k < (16 + 8 * hd.nb + 15) / 16; k += FT)
           reinterpret_cast<uint4*>(tbl)[k] = reinterpret_cast<const uint4*>(epi_table)[k];
-        tb = EpiLds{tbl + sizeof(EpiTableHdr), hd.c0, hd.inv_w, (float)(hd.nb - 1)};
+        tb = EpiLds{tbl + sizeof(EpiTableHdr), hd.c0, hd.inv_w, epi_top(hd.nb)};
       }
     }
   }
@@ -190,7 +190,7 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
         acc[0][f] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wf, xa[q][0], acc[0][f], 0, 0, 0);
         acc[1][f] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wf, xa[q][1], acc[1][f], 0, 0, 0);  // tile may be past N
       }
-      sp.mark(1);
+      sp.mark(8);
       ++g;
     };
     for (int s = 0; s < nk; s += 4) {
@@ -201,7 +201,7 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
     }
     cur = nxt;
     unit_src(j + 2, nxt);
-    sp.mark(2);
+    sp.mark(9);
 
     // ---- 2. epilogue: q -> registers, k / v -> LDS images -----------------------------------------
     // acc[tt][4p + r][jj] = feature 64h + 16 fq + 4 r + jj of group p (q, k, v) for token 16 tile + fr
@@ -245,7 +245,7 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
       }
     }
     __syncthreads();  // K / V images complete
-    sp.mark(2);
+    sp.mark(9);
 
     // ---- 3. attention over the resident K / V ------------------------------------------------------
     float m[TPW], l[TPW];
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
         attend<TPW, IMGF>(nt, (kb + 1) * KB > N, kv + kb * KB * 128, qh, ql, m, l, o, koffs, voffs, kb * KB + 4 * fq,
                           N, sl2, sp);
     }
-    sp.mark(3);
+    sp.mark(0);
     attend_store<OUT, TPW>(tv, l, o, wr, FW, 0, N, b, h, in_scale, out, ldo, qp, tb, st16);
     sp.mark(4);
   }

@@ -311,7 +311,7 @@ __global__ __launch_bounds__(kThreads) void layernorm_quant_persist_kernel(
   const int lane = threadIdx.x & 63;
   const int tid = threadIdx.x;
   const int8_t* ent = nullptr;
-  float c0 = 0.f, inv_w = 0.f, nbm1 = 0.f;
+  float c0 = 0.f, inv_w = 0.f, top = 0.f;
   if (table != nullptr) {
     const EpiTableHdr hd = *reinterpret_cast<const EpiTableHdr*>(table);
     if (hd.valid != 0 && hd.nb >= 1 && 16 + 8 * hd.nb <= LN_TBL_BYTES) {
@@ -320,7 +320,7 @@ __global__ __launch_bounds__(kThreads) void layernorm_quant_persist_kernel(
       ent = tl + sizeof(EpiTableHdr);
       c0 = hd.c0;
       inv_w = hd.inv_w;
-      nbm1 = (float)(hd.nb - 1);
+      top = epi_top(hd.nb);
     }
   }
   __syncthreads();
@@ -373,7 +373,7 @@ __global__ __launch_bounds__(kThreads) void layernorm_quant_persist_kernel(
           uint2 e[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            e[j] = *reinterpret_cast<const uint2*>(ent + (epi_bucket(y[j], c0, inv_w, nbm1) << 3));
+            e[j] = *epi_entry(ent, y[j], c0, inv_w, top);
           epi_select_byte<0>(word, y[0], __uint_as_float(e[0].x), e[0].y);
           epi_select_byte<1>(word, y[1], __uint_as_float(e[1].x), e[1].y);
           epi_select_byte<2>(word, y[2], __uint_as_float(e[2].x), e[2].y);

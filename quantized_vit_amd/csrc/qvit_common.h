@@ -132,7 +132,7 @@ QVIT_DEV int8_t to_i8_sat(float k) {
 // ---- code tables of the int8 epilogues (qvit_epi_table_build; GEMM and attention epilogues) ----------
 // header (16 B) + nb entries {thr, lo | hi << 8} (8 B each); see gemm_w4a8.hip for the construction.
 struct EpiTableHdr {
-  float c0;     // -v_lo * inv_w (rounded): bucket(v) = clamp(int(fma(v, inv_w, c0)), 0, nb - 1)
+  float c0;     // C = 2^23 + (-v_lo * inv_w), rounded: see epi_bucket_bits
   float inv_w;
   int nb;
   int valid;
@@ -142,9 +142,20 @@ struct EpiTableEnt {
   int8_t lo, hi;
   int16_t pad;
 };
-// Monotone in v (the bisection in the builder relies on it); one FMA and one med3 in the epilogue.
-QVIT_DEV int epi_bucket(float v, float c0, float inv_w, float nbm1) {
-  return (int)__builtin_amdgcn_fmed3f(fmaf(v, inv_w, c0), 0.f, nbm1);
+// Bucket of v: f = med3(fma(v, inv_w, C), 2^23, 2^23 + nb - 1). In [2^23, 2^24) a float's ulp is 1, so the
+// fma itself rounds to the bucket index, which then sits in f's low mantissa bits: bits(f) = 0x4B000000 + j.
+// Monotone in v (the builder's bisection relies on it); one FMA and one med3, no float->int conversion,
+// and the entry's byte offset is one shift-add of bits(f).
+QVIT_DEV float epi_top(int nb) { return 8388608.f + (float)(nb - 1); }
+QVIT_DEV uint32_t epi_bucket_bits(float v, float C, float inv_w, float top) {
+  return __float_as_uint(__builtin_amdgcn_fmed3f(fmaf(v, inv_w, C), 8388608.f, top));
+}
+QVIT_DEV int epi_bucket(float v, float C, float inv_w, float top) {
+  return (int)(epi_bucket_bits(v, C, inv_w, top) - 0x4B000000u);
+}
+// v's 8-B entry in an LDS-resident table whose entries start at `ent`
+QVIT_DEV const uint2* epi_entry(const int8_t* ent, float v, float C, float inv_w, float top) {
+  return reinterpret_cast<const uint2*>(ent + ((epi_bucket_bits(v, C, inv_w, top) << 3) - (0x4B000000u << 3)));
 }
 
 // wd.byte[J] = (v >= thr) ? byte 1 of lohi : byte 0 of lohi (J = 0 also zeroes bytes 1..3):

@@ -109,8 +109,9 @@ def main():
             torch.cuda.synchronize()
             assert lib.qvit_qkv_att_stamps(buf, 0) == 0
             waves = max(buf[15], 1)
-            per = [buf[i] / waves for i in range(8)]
-            names = ["-", "proj reads+mfma", "epilogue", "attention", "store", "load issue", "w write(wait)", "barrier"]
+            per = [buf[i] / waves for i in range(10)]
+            names = ["attn tail", "scores", "softmax", "PV", "store", "load issue", "w write(wait)", "barrier",
+                     "proj reads+mfma", "proj epilogue"]
             tot = sum(per)
             print("fused per wave: " + "  ".join(f"{n} {v:8.0f} ({100*v/tot:4.1f}%)" for n, v in zip(names, per)))
     if a.split_only:
