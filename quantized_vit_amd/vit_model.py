@@ -350,22 +350,35 @@ class VisionTransformer(nn.Module):
 
     def forward_features(self, x):
         x = self.patch_embed(x)
-        cls_token = self.cls_token.expand(x.shape[0], -1, -1)
-        if self.dist_token is None:
-            x = torch.cat((cls_token, x), dim=1)
+        if x.is_cuda and _inactive(self.pos_drop):
+            # cat((cls[, dist], x)) + pos_embed in one pass: the token rows are written straight into the
+            # residual buffer (the same fp32 additions as the reference's cat-then-add)
+            B, T, C = x.shape
+            nt = self.num_tokens
+            buf = torch.empty((B, T + nt, C), dtype=x.dtype, device=x.device)
+            torch.add(x, self.pos_embed[:, nt:], out=buf[:, nt:])
+            buf[:, 0] = self.cls_token[:, 0] + self.pos_embed[:, 0]
+            if self.dist_token is not None:
+                buf[:, 1] = self.dist_token[:, 0] + self.pos_embed[:, 1]
+            x = buf
         else:
-            x = torch.cat((cls_token, self.dist_token.expand(x.shape[0], -1, -1), x), dim=1)
-        x = self.pos_drop(x + self.pos_embed)
+            cls_token = self.cls_token.expand(x.shape[0], -1, -1)
+            if self.dist_token is None:
+                x = torch.cat((cls_token, x), dim=1)
+            else:
+                x = torch.cat((cls_token, self.dist_token.expand(x.shape[0], -1, -1), x), dim=1)
+            x = self.pos_drop(x + self.pos_embed)
         # the residual stream is a fresh buffer here, so fused blocks may update it in place
         for blk in self.blocks:
             if isinstance(blk, Block) and blk.fused_ok(x):
                 x = blk.forward_fused_(x.contiguous())
             else:
                 x = blk(x)
-        x = self.norm(x)
+        # LayerNorm is per token: only the class (and distillation) token rows reach the heads
         if self.dist_token is None:
-            return self.pre_logits(x[:, 0])
+            return self.pre_logits(self.norm(x[:, 0]))
         else:
+            x = self.norm(x[:, :2])
             return x[:, 0], x[:, 1]
 
     def forward(self, x):
