@@ -52,11 +52,14 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(model, x_gpu_logits_fn, img_size: int, batch: int, iters: int):
+def cpu_baseline(model, model_name: str, x_gpu_logits_fn, img_size: int, batch: int, iters: int):
     """Times the oracle's fp32 fake-quant forward on the host cores (bounded sample) and checks the
     GPU logits on the same images against it."""
     from oracle import quant_oracle as O
-    cfg = O.ViTConfig()
+    from quantized_vit_amd.calibrate import VIT_CONFIGS
+    mc = VIT_CONFIGS[model_name]
+    cfg = O.ViTConfig(img_size=mc["img_size"], patch_size=mc["patch_size"], embed_dim=mc["embed_dim"],
+                      depth=mc["depth"], num_heads=mc["num_heads"])
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
     img = synthetic_images(batch, img_size, seed=12345)
     torch.set_num_threads(max(1, torch.get_num_threads()))
@@ -87,7 +90,7 @@ def cpu_baseline(model, x_gpu_logits_fn, img_size: int, batch: int, iters: int):
         pass
     return {
         "value": batch / med, "unit": "img/s", "cores": torch.get_num_threads(), "kind": "port",
-        "sample": f"oracle fp32 fake-quant ViT-B/16 forward, batch {batch}, median of {iters} after 1 warm-up "
+        "sample": f"oracle fp32 fake-quant {model_name} forward, batch {batch}, median of {iters} after 1 warm-up "
                   f"({cpu_model})",
     }, rel, floor
 
@@ -187,7 +190,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         def gpu_logits(img):
             return model(img.to(dev)).cpu()
-        cb, rel, floor = cpu_baseline(model, gpu_logits, img_size, args.cpu_batch, args.cpu_iters)
+        cb, rel, floor = cpu_baseline(model, args.model, gpu_logits, img_size, args.cpu_batch, args.cpu_iters)
         result["cpu_baseline"] = cb
         result["parity_rel_err_vs_oracle"] = rel
         result["parity_oracle_fp32_vs_fp64"] = floor

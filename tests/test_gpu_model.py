@@ -353,3 +353,28 @@ def test_pruned_shapes_vs_oracle(dev):
         y = m(img.to(dev))
     cfg = O.ViTConfig(embed_dim=192, depth=2, num_heads=3, num_classes=37)
     check_vit_parity(m, cfg, img, dev)
+
+
+def test_vit_large_384_stage_forced(dev):
+    """BASELINE config 4 (ViT-L/16 @384: 577 tokens, embed 1024, 16 heads): the sequence is longer than
+    the fused qkv+attention kernel holds, so the blocks take the split-operand path (qkv GEMM to fp16
+    hi/lo head planes + the streaming attention kernel). Two blocks, stage by stage against the oracle
+    (bars as for ViT-B), plus the end-to-end logits against the fp64-vs-fp32 floor."""
+    model = build_quantized_vit("vit_large_patch16_384", seed=0, depth=2).to(dev)
+    cfg = O.ViTConfig(img_size=384, embed_dim=1024, depth=2, num_heads=16)
+    img = synthetic_images(1, 384, seed=5)
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    trace = []
+    with torch.no_grad():
+        ref32 = O.vit_forward(sd, cfg, img, trace=trace)
+        ref64 = O.vit_forward({k: v.double() for k, v in sd.items()}, cfg, img.double())
+        assert trace[0].shape[1] == 577
+        for i in range(cfg.depth):
+            for name, r in stage_forced_block(model, cfg, sd, trace[i], i, dev).items():
+                if r[0] == "fp32":
+                    assert r[1] <= 1e-6, (i, name, r)
+                else:
+                    assert r[1] <= (1e-5 if "weight" in name else 1e-4) and r[2] <= 1, (i, name, r)
+        y = model(img.to(dev))
+    floor = rel(ref64, ref32)
+    assert rel(y, ref32) <= 2.5 * floor + 1e-4, (rel(y, ref32), floor)
