@@ -240,6 +240,24 @@ int qvit_ultra_conv(const int8_t* in, int64_t B, int64_t H, int64_t W, int64_t c
                     const int8_t* wcodes, int64_t kpad, int64_t cout, int w_bit, int a_bit,
                     const float* alpha, const float* shift, int mode, void* out, int64_t ldo,
                     hipStream_t stream);
+/*
+ * UltraNet integer deploy (reference `4-bit quantization/`: quantization.py:24-31,68-89,
+ * qnn_param_reader.py:58-85, ultranet_param_gen.py:14-22 — the FPGA flow's integer parameters):
+ *   code = clamp(round((acc * inc_q[o] + bias_q[o]) / 2^S), 0, 2^out_bit - 1), round half up, 64-bit
+ *   intermediate, S = w_bit - 1 + in_bit + l_shift; inc_q / bias_q from bn_act_quantize_int (host side).
+ *   Replaces the accelerator's conv + BN + activation stage (its HLS source is absent from the reference;
+ *   the rounding shown is the float path's round(), restated in integers: parity unpinned beyond it).
+ * qvit_ultra_conv0_int: layer 0 on uint8 pixels NCHW [B][3][H][W] (in_bit 8), weight codes [16][3][3][3]
+ *   (reference layout, weight_quantize_int) -> 2x2 max-pooled codes NHWC [B][H/2][W/2][16] (16-B aligned).
+ * qvit_ultra_conv_int: layers 1..7 as qvit_ultra_conv (same input / weight layouts and shapes, 3x3 only)
+ *   with the integer threshold; pool != 0 adds MaxPool2d(2, 2) on the codes.
+ */
+int qvit_ultra_conv0_int(const uint8_t* img, int64_t B, int64_t H, int64_t W, const int8_t* wcodes,
+                         const int32_t* inc, const int32_t* bias, int shift_bits, int out_bit, int8_t* out,
+                         hipStream_t stream);
+int qvit_ultra_conv_int(const int8_t* in, int64_t B, int64_t H, int64_t W, int64_t cin, int64_t ks,
+                        const int8_t* wcodes, int64_t kpad, int64_t cout, const int32_t* inc, const int32_t* bias,
+                        int shift_bits, int out_bit, int pool, int8_t* out, int64_t ldo, hipStream_t stream);
 int qvit_yolo_decode(const float* head, int64_t B, int64_t ny, int64_t nx, int64_t na, int64_t no,
                      int64_t ldh, const float* anchors, float stride, float* io, float* p,
                      hipStream_t stream);

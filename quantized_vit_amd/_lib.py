@@ -67,6 +67,9 @@ _SIGNATURES = {
     "qvit_ultra_conv0": [_c_p, _i64, _i64, _i64, _c_p, _c_p, _c_p, _i32, _c_p, _c_p],
     "qvit_ultra_conv": [_c_p, _i64, _i64, _i64, _i64, _i64, _c_p, _i64, _i64, _i32, _i32, _c_p, _c_p, _i32, _c_p,
                         _i64, _c_p],
+    "qvit_ultra_conv0_int": [_c_p, _i64, _i64, _i64, _c_p, _c_p, _c_p, _i32, _i32, _c_p, _c_p],
+    "qvit_ultra_conv_int": [_c_p, _i64, _i64, _i64, _i64, _i64, _c_p, _i64, _i64, _c_p, _c_p, _i32, _i32, _i32,
+                            _c_p, _i64, _c_p],
     "qvit_yolo_decode": [_c_p, _i64, _i64, _i64, _i64, _i64, _i64, _c_p, _f32, _c_p, _c_p, _c_p],
     "qvit_attention": [_c_p, _i64, _i64, _i64, _i64, _i64, _f32, _f32, _i32, _c_p, _i64, _i32, _c_p, _c_p, _c_p,
                        _i32, _c_p],
@@ -333,6 +336,36 @@ def ultra_conv(x: torch.Tensor, ks: int, wcodes: torch.Tensor, cout: int, w_bit:
     _check(load().qvit_ultra_conv(_ptr(x), B, H, W, cin, ks, _ptr(wcodes), wcodes.shape[1], cout, w_bit, a_bit,
                                   _ptr(alpha), _ptr(shift), mode, _ptr(out), cout, _stream(x.device)),
            "qvit_ultra_conv")
+    return out
+
+
+def ultra_conv0_int(img_u8: torch.Tensor, wcodes: torch.Tensor, inc: torch.Tensor, bias: torch.Tensor,
+                    shift_bits: int, out_bit: int) -> torch.Tensor:
+    """Integer deploy layer 0: uint8 image NCHW -> conv3x3 (weight codes [16][3][3][3]) -> integer BN/act
+    threshold -> 2x2 max pool -> NHWC codes [B][H/2][W/2][16]."""
+    _require_gpu(img_u8, "image")
+    assert img_u8.dtype == torch.uint8 and img_u8.is_contiguous() and img_u8.shape[1] == 3
+    assert wcodes.shape == (16, 3, 3, 3) and wcodes.dtype == torch.int8 and wcodes.is_contiguous()
+    assert inc.dtype == torch.int32 and bias.dtype == torch.int32 and inc.numel() >= 16 and bias.numel() >= 16
+    B, _, H, W = img_u8.shape
+    out = torch.empty((B, H // 2, W // 2, 16), dtype=torch.int8, device=img_u8.device)
+    _check(load().qvit_ultra_conv0_int(_ptr(img_u8), B, H, W, _ptr(wcodes), _ptr(inc), _ptr(bias), shift_bits,
+                                       out_bit, _ptr(out), _stream(img_u8.device)), "qvit_ultra_conv0_int")
+    return out
+
+
+def ultra_conv_int(x: torch.Tensor, ks: int, wcodes: torch.Tensor, cout: int, inc: torch.Tensor, bias: torch.Tensor,
+                   shift_bits: int, out_bit: int, pool: bool) -> torch.Tensor:
+    """Integer deploy layers 1..7: NHWC codes [B][H][W][cin] -> NHWC codes (2x2 max-pooled when pool)."""
+    _require_gpu(x, "codes")
+    assert x.dtype == torch.int8 and x.is_contiguous()
+    assert inc.dtype == torch.int32 and bias.dtype == torch.int32 and inc.numel() >= cout and bias.numel() >= cout
+    B, H, W, cin = x.shape
+    shape = (B, H // 2, W // 2, cout) if pool else (B, H, W, cout)
+    out = torch.empty(shape, dtype=torch.int8, device=x.device)
+    _check(load().qvit_ultra_conv_int(_ptr(x), B, H, W, cin, ks, _ptr(wcodes), wcodes.shape[1], cout, _ptr(inc),
+                                      _ptr(bias), shift_bits, out_bit, 1 if pool else 0, _ptr(out), cout,
+                                      _stream(x.device)), "qvit_ultra_conv_int")
     return out
 
 

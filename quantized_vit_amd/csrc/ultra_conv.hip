@@ -133,6 +133,71 @@ __global__ __launch_bounds__(256) void ultra_conv0_kernel(const float* __restric
   }
 }
 
+// ---- integer deploy (quantization.py:24-31,68-89; ultranet_param_gen.py) --------------------------------
+// The FPGA flow's integer form of conv -> BN -> activation quantizer: with per-channel inc_q, bias_q from
+// bn_act_quantize_int and S = w_bit - 1 + in_bit + l_shift,
+//   code = clamp(round((acc * inc_q + bias_q) / 2^S), 0, 2^out_bit - 1),   round = half up ((x + 2^(S-1)) >> S)
+// in 64-bit integer arithmetic (acc * inc_q can exceed 32 bits). The accelerator's own rounding is not in
+// the reference (its HLS source is absent): parity for this formula is unpinned beyond the oracle's
+// restatement of the same expression.
+QVIT_DEV int int_code(int acc, int inc, int bias, int sbits, int levels) {
+  const long long v = ((long long)acc * inc + bias + (1ll << (sbits - 1))) >> sbits;
+  return (int)(v < 0 ? 0 : (v > levels ? levels : v));
+}
+
+// Layer 0 of the integer deploy: uint8 image NCHW (in_bit 8), weight codes [16][3][3][3] (reference layout),
+// int32 accumulation, integer threshold, 2x2 max pool on the codes -> NHWC codes [B][H/2][W/2][16].
+__global__ __launch_bounds__(256) void ultra_conv0_int_kernel(const uint8_t* __restrict__ img, int B, int H, int W,
+                                                              const int8_t* __restrict__ wcodes,
+                                                              const int* __restrict__ inc,
+                                                              const int* __restrict__ bias, int sbits, int levels,
+                                                              int8_t* __restrict__ out) {
+  const int Ho = H / 2, Wo = W / 2;
+  const int64_t total = (int64_t)B * Ho * Wo;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int xo = (int)(i % Wo);
+    const int yo = (int)((i / Wo) % Ho);
+    const int b = (int)(i / ((int64_t)Wo * Ho));
+    int win[C0_IN][4][4];
+#pragma unroll
+    for (int c = 0; c < C0_IN; ++c)
+#pragma unroll
+      for (int dy = 0; dy < 4; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 4; ++dx) {
+          const int y = 2 * yo - 1 + dy, x = 2 * xo - 1 + dx;
+          win[c][dy][dx] = (y >= 0 && y < H && x >= 0 && x < W) ? img[(((int64_t)b * C0_IN + c) * H + y) * W + x] : 0;
+        }
+    uint32_t words[4] = {0, 0, 0, 0};
+#pragma unroll 1
+    for (int o = 0; o < C0_OUT; ++o) {
+      const int8_t* wo = wcodes + o * C0_K;  // [c][ky][kx], wave-uniform
+      int a00 = 0, a01 = 0, a10 = 0, a11 = 0;
+#pragma unroll
+      for (int c = 0; c < C0_IN; ++c)
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) {
+            const int wv = wo[(c * 3 + ky) * 3 + kx];
+            a00 += wv * win[c][ky][kx];
+            a01 += wv * win[c][ky][kx + 1];
+            a10 += wv * win[c][ky + 1][kx];
+            a11 += wv * win[c][ky + 1][kx + 1];
+          }
+      const int ic = inc[o], bc = bias[o];
+      const int best = max(max(int_code(a00, ic, bc, sbits, levels), int_code(a01, ic, bc, sbits, levels)),
+                           max(int_code(a10, ic, bc, sbits, levels), int_code(a11, ic, bc, sbits, levels)));
+      const uint32_t v = (uint32_t)best << (8 * (o & 3));
+      if ((o >> 2) == 0) words[0] |= v;
+      else if ((o >> 2) == 1) words[1] |= v;
+      else if ((o >> 2) == 2) words[2] |= v;
+      else words[3] |= v;
+    }
+    *reinterpret_cast<uint4*>(out + i * C0_OUT) = make_uint4(words[0], words[1], words[2], words[3]);
+  }
+}
+
 // ---- layers 1..8: implicit GEMM conv on MFMA ------------------------------------------------------
 constexpr int TS = 16;  // output tile 16 x 16 (pre-pool) pixels
 
@@ -147,13 +212,15 @@ struct ConvGeo {
   static constexpr int NCT = COUT / 16;
 };
 
-// OUT: 0 = BN + quantizer codes (POOL: + 2x2 max pool), 1 = acc/den + bias fp32
+// OUT: 0 = BN + quantizer codes (POOL: + 2x2 max pool), 1 = acc/den + bias fp32,
+//      2 = integer deploy threshold (alpha / shift hold int32 inc_q / bias_q, sbits = S; POOL as for 0)
 template <int CIN, int KS, int COUT, int POOL, int OUT>
 __global__ __launch_bounds__(256, 2) void ultra_conv_kernel(const int8_t* __restrict__ in, int B, int H, int W,
                                                             const int8_t* __restrict__ wcodes, int kpad_in,
                                                             float den, const float* __restrict__ alpha,
                                                             const float* __restrict__ shift, float levels,
-                                                            int cout_real, void* __restrict__ out, int ldo) {
+                                                            int cout_real, void* __restrict__ out, int ldo,
+                                                            int sbits) {
   using G = ConvGeo<CIN, KS, COUT>;
   __shared__ __attribute__((aligned(16))) int8_t smem[G::LDS];
   int8_t* wl = smem;
@@ -171,13 +238,16 @@ __global__ __launch_bounds__(256, 2) void ultra_conv_kernel(const int8_t* __rest
         *reinterpret_cast<const v4i*>(wcodes + (int64_t)o * kpad_in + 16 * c16);
   }
   float al[G::NCT][4], sh[G::NCT][4];
+  int iinc[G::NCT][4], ibias[G::NCT][4];
 #pragma unroll
   for (int ct = 0; ct < G::NCT; ++ct)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int o = 16 * ct + 4 * g + j;
       al[ct][j] = (OUT == 0 && o < cout_real) ? alpha[o] : 0.f;
-      sh[ct][j] = (o < cout_real) ? shift[o] : 0.f;  // OUT == 1: shift = bias
+      sh[ct][j] = (OUT != 2 && o < cout_real) ? shift[o] : 0.f;  // OUT == 1: shift = bias
+      iinc[ct][j] = (OUT == 2 && o < cout_real) ? reinterpret_cast<const int*>(alpha)[o] : 0;
+      ibias[ct][j] = (OUT == 2 && o < cout_real) ? reinterpret_cast<const int*>(shift)[o] : 0;
     }
 
   const int tiles_y = (H + TS - 1) / TS, tiles_x = (W + TS - 1) / TS;
@@ -243,7 +313,9 @@ __global__ __launch_bounds__(256, 2) void ultra_conv_kernel(const int8_t* __rest
         } else {
           int code[4];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) code[j] = act_code((float)acc[pt][ct][j] / den, al[ct][j], sh[ct][j], levels);
+          for (int j = 0; j < 4; ++j)
+            code[j] = (OUT == 2) ? int_code(acc[pt][ct][j], iinc[ct][j], ibias[ct][j], sbits, (int)levels)
+                                 : act_code((float)acc[pt][ct][j] / den, al[ct][j], sh[ct][j], levels);
           if (POOL) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -304,13 +376,14 @@ int grid_cap(int64_t work, int per = 256) {
 
 template <int CIN, int KS, int COUT, int POOL, int OUT>
 int launch_conv(const int8_t* in, int B, int H, int W, const int8_t* w, int kpad, float den, const float* alpha,
-                const float* shift, float levels, int cout_real, void* out, int ldo, hipStream_t stream) {
+                const float* shift, float levels, int cout_real, void* out, int ldo, hipStream_t stream,
+                int sbits = 0) {
   using G = ConvGeo<CIN, KS, COUT>;
   if (kpad < G::KPAD) return QVIT_EINVAL;
   const int64_t ntiles = (int64_t)B * ((H + TS - 1) / TS) * ((W + TS - 1) / TS);
   const int grid = (int)(ntiles < 256 * 8 ? ntiles : 256 * 8);
   hipLaunchKernelGGL((ultra_conv_kernel<CIN, KS, COUT, POOL, OUT>), dim3(grid), dim3(256), 0, stream, in, B, H, W,
-                     w, kpad, den, alpha, shift, levels, cout_real, out, ldo);
+                     w, kpad, den, alpha, shift, levels, cout_real, out, ldo, sbits);
   return qvit_hip_status(hipGetLastError());
 }
 
@@ -386,6 +459,51 @@ extern "C" int qvit_ultra_conv(const int8_t* in, int64_t B, int64_t H, int64_t W
   QVIT_ULTRA_CASE(64, 1, 48)
 #undef QVIT_ULTRA_CASE
   return QVIT_EINVAL;  // shapes outside UltraNetQua's layer set
+}
+
+extern "C" int qvit_ultra_conv0_int(const uint8_t* img, int64_t B, int64_t H, int64_t W, const int8_t* wcodes,
+                                    const int32_t* inc, const int32_t* bias, int shift_bits, int out_bit, int8_t* out,
+                                    hipStream_t stream) {
+  if (!img || !wcodes || !inc || !bias || !out) return QVIT_ENULL;
+  if (B < 0 || H < 2 || W < 2 || shift_bits < 1 || shift_bits > 40 || out_bit < 1 || out_bit > 7) return QVIT_EINVAL;
+  if ((((uintptr_t)out) & 15)) return QVIT_EALIGN;
+  if (B * H * W > INT32_MAX) return QVIT_EINVAL;
+  if (B == 0) return QVIT_OK;
+  const int64_t work = B * (H / 2) * (W / 2);
+  hipLaunchKernelGGL(ultra_conv0_int_kernel, dim3(grid_cap(work)), dim3(256), 0, stream, img, (int)B, (int)H, (int)W,
+                     wcodes, inc, bias, shift_bits, (1 << out_bit) - 1, out);
+  return qvit_hip_status(hipGetLastError());
+}
+
+extern "C" int qvit_ultra_conv_int(const int8_t* in, int64_t B, int64_t H, int64_t W, int64_t cin, int64_t ks,
+                                   const int8_t* wcodes, int64_t kpad, int64_t cout, const int32_t* inc,
+                                   const int32_t* bias, int shift_bits, int out_bit, int pool, int8_t* out, int64_t ldo,
+                                   hipStream_t stream) {
+  if (!in || !wcodes || !inc || !bias || !out) return QVIT_ENULL;
+  if (B < 0 || H < 1 || W < 1 || cout < 1 || ldo < cout || shift_bits < 1 || shift_bits > 40 || out_bit < 1 ||
+      out_bit > 7)
+    return QVIT_EINVAL;
+  if (pool && ((H | W) & 1)) return QVIT_EINVAL;
+  if ((((uintptr_t)in) & 15) || (((uintptr_t)wcodes) & 15) || (kpad % 16)) return QVIT_EALIGN;
+  if (ldo % 4 || (((uintptr_t)out) & 3) || cout % 4 || (((uintptr_t)inc) & 3) || (((uintptr_t)bias) & 3))
+    return QVIT_EALIGN;
+  if (B * H * W > INT32_MAX) return QVIT_EINVAL;
+  if (B == 0) return QVIT_OK;
+  const float lv = (float)((1 << out_bit) - 1);
+  const float* fi = reinterpret_cast<const float*>(inc);
+  const float* fb = reinterpret_cast<const float*>(bias);
+  const int b = (int)B, h = (int)H, w = (int)W, co = (int)cout, ld = (int)ldo, kp = (int)kpad;
+#define QVIT_ULTRA_INT_CASE(CI, K, CO)                                                                               \
+  if (cin == CI && ks == K && cout <= CO && cout > CO - 16) {                                                      \
+    if (pool)                                                                                                      \
+      return launch_conv<CI, K, CO, 1, 2>(in, b, h, w, wcodes, kp, 1.f, fi, fb, lv, co, out, ld, stream, shift_bits); \
+    return launch_conv<CI, K, CO, 0, 2>(in, b, h, w, wcodes, kp, 1.f, fi, fb, lv, co, out, ld, stream, shift_bits);   \
+  }
+  QVIT_ULTRA_INT_CASE(16, 3, 32)
+  QVIT_ULTRA_INT_CASE(32, 3, 64)
+  QVIT_ULTRA_INT_CASE(64, 3, 64)
+#undef QVIT_ULTRA_INT_CASE
+  return QVIT_EINVAL;  // shapes outside UltraNetQua's quantized layer set
 }
 
 extern "C" int qvit_yolo_decode(const float* head, int64_t B, int64_t ny, int64_t nx, int64_t na, int64_t no,

@@ -144,3 +144,51 @@ def test_ultra_argument_validation(dev):
     # codes mode needs BN alpha
     assert lib.qvit_ultra_conv(x.data_ptr(), 1, 8, 8, 16, 3, w.data_ptr(), 448, 32, 4, 4, None, a.data_ptr(),
                                0, out.data_ptr(), 32, s) == -3
+
+
+# ---- integer deploy (F4: quantization.py integer parameters, ultranet_param_gen.py bit widths) --------
+@pytest.mark.parametrize("size,batch", [(64, 2), (96, 1)])
+def test_int_deploy_vs_oracle(dev, size, batch):
+    """Every layer's integer codes identical to the oracle's integer restatement (the same npz read the
+    reference's way), the head's fp32 output bit-identical, and the YOLO decode within 1e-6."""
+    import numpy as np
+    from oracle import quantization_np as Q
+    from quantized_vit_amd import convert
+    from quantized_vit_amd.ultra_deploy import UltraNetIntDeploy
+    model = random_ultranet(seed=3, device=dev, calib_batch=2, img_size=size)
+    arrs = convert.ultranet_to_npz(model)
+    dep = UltraNetIntDeploy(arrs, dev)
+    img = (synthetic_images_u8(batch, size, seed=11) * 255).round().to(torch.uint8)
+    feats = dep.features(img.to(dev))
+    for b in range(batch):
+        ref = Q.ultranet_int_forward(arrs, img[b].numpy())
+        for i, (g, r) in enumerate(zip(feats[:-1], ref[:-1])):
+            got = g[b].cpu().to(torch.int64).permute(2, 0, 1).numpy()
+            assert got.shape == r.shape, (i, got.shape, r.shape)
+            assert np.array_equal(got, r), (i, int((got != r).sum()))
+            if i < 7:
+                assert 0 < r.max() and r.min() < 15   # the codes spread over the range
+        head = feats[-1][b].cpu().permute(2, 0, 1).numpy()
+        assert np.array_equal(head, ref[-1]), float(np.abs(head - ref[-1]).max())
+    io, p = dep(img.to(dev))
+    io_ref, _ = dep.yolo(torch.from_numpy(np.stack([Q.ultranet_int_forward(arrs, img[b].numpy())[-1]
+                                                    for b in range(batch)])).to(dev), img.shape[-2:])
+    assert rel(io, io_ref) <= 1e-6
+
+
+def test_int_deploy_argument_validation(dev):
+    lib = _lib.load()
+    x = torch.zeros(16 * 16 * 16 * 16, dtype=torch.int8, device=dev)
+    w = torch.zeros(32 * 192, dtype=torch.int8, device=dev)
+    i32 = torch.zeros(64, dtype=torch.int32, device=dev)
+    s = _lib._stream(dev)
+
+    def call(**kw):
+        a = dict(inp=x.data_ptr(), B=1, H=16, W=16, cin=16, ks=3, w=w.data_ptr(), kpad=192, cout=32,
+                 inc=i32.data_ptr(), bias=i32.data_ptr(), sb=15, ob=4, pool=1, out=x.data_ptr(), ldo=32)
+        a.update(kw)
+        return lib.qvit_ultra_conv_int(*a.values(), s)
+    assert call() == 0
+    assert call(sb=0) == -1 and call(ob=8) == -1 and call(cin=24) == -1 and call(H=15) == -1
+    assert call(inc=None) == -3 and call(inp=x.data_ptr() + 4) == -2
+    torch.cuda.synchronize()
