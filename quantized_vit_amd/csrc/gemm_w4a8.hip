@@ -478,6 +478,10 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     // ---- epilogue (epilogue LDS region only; the next tile's DMA streams underneath) -----------
     // acc[r][s][j] = C[m0 + 128 wm + 16 s + fr][n0 + 64 wn + 16 fq + 4 r + j] (weight rows pre-permuted)
     const int el = lane_opaque();
+    // the int8 epilogue (VALU + LDS lookups) runs at raised wave priority: the co-resident block's
+    // main loop keeps the matrix pipe busy either way, and the epilogue no longer loses every issue
+    // arbitration to it (fc1: -9 % time; the fp32 epilogues wait on memory and gain nothing)
+    if (I8OUT) __builtin_amdgcn_s_setprio(1);
     const int efr = el & 15, efq = el >> 4;
     if (I8OUT && use_table) {
       // register path: lane (fr, fq) owns the 16 consecutive columns [nbase, nbase+16) of rows
@@ -700,6 +704,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
       }
     }
     }
+    if (I8OUT) __builtin_amdgcn_s_setprio(0);
     QVIT_STAMP(4);
     if (!has_next) break;
     t = tnext;
