@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--cpu-batch", type=int, default=8)
     ap.add_argument("--cpu-iters", type=int, default=3)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--lib", default="", help=argparse.SUPPRESS)  # diagnostic: A/B another build of the library
     return ap.parse_args()
 
 
@@ -108,7 +109,7 @@ def main():
         qbuild.build()
     if world > 1:
         dist.barrier()
-    _lib.load()
+    _lib.load(args.lib) if args.lib else _lib.load()
 
     img_size = {"vit_base_patch16_224": 224, "vit_large_patch16_384": 384, "vit_tiny_patch16_224": 224}[args.model]
     model = build_quantized_vit(args.model, seed=args.seed, device=dev)

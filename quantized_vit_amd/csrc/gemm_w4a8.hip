@@ -100,6 +100,21 @@ QVIT_DEV void dma16(const void* gsrc, uint32_t lds_base) {
       : "memory");
 }
 
+// The same from a wave-uniform SGPR base + a per-lane 32-bit byte offset (the global "saddr" form): no
+// 64-bit per-lane address arithmetic and no VGPR pair holding a base pointer across the main loop.
+QVIT_DEV void dma16s(const void* sbase, uint32_t voff, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(lds_base)
+      : "memory");
+}
+
 // Wait until at most N of this wave's DMAs are in flight, retire its LDS reads, then barrier.
 // The LDS drain is the builtin (lgkmcnt(0) = 0xC07F on gfx9) so the compiler's wait-count model sees
 // it and does not re-drain lgkmcnt when the next stage's fragment reads are in flight.
@@ -285,7 +300,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   float alpha = 0.f;
   if (EPI != QVIT_EPI_I32) alpha = (*ep.d_act) * (*ep.d_wt) * (WFMT == QVIT_W4 ? 0.0625f : 1.f);
   bool use_table = false;
-  float t_c0 = 0.f, t_invw = 0.f, t_top = 0.f;
+  float t_c0 = 0.f, t_invw = 0.f, t_top = 0.f;  // wave-uniform (SGPRs)
   int t_nb = 1;
   if (I8OUT && ep.table != nullptr) {
     const EpiTableHdr h = *reinterpret_cast<const EpiTableHdr*>(ep.table);
@@ -310,13 +325,14 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   constexpr int WROWS_PER_WAVE = BN / G::NWAVES;
   const int nk = K / BK;  // even, >= 2
   // a tile's sources are uniform (m0, weight-tile base); the per-lane parts are tile-invariant
+  // byte offsets from the A / Wp kernel arguments fit 32 bits (checked by the launcher)
   struct Src {
     int m0;
-    const int8_t* w;
+    uint32_t w;  // the weight tile's byte offset in Wp
   };
   auto tile_src = [&](int tt, Src& sr) {
     sr.m0 = (tt / nb_n) * BM;
-    sr.w = Wp + (int64_t)(tt % nb_n) * nk * G::WBYTES;
+    sr.w = (uint32_t)(tt % nb_n) * (uint32_t)(nk * G::WBYTES);
   };
   const uint32_t lds0 = lds_addr(smem);
   auto issue = [&](const Src& sr, int kt, int rslot) {
@@ -325,27 +341,30 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
 #endif
     const uint32_t sx = lds0 + (uint32_t)(rslot * G::STAGE);
     const uint32_t sw = sx + XBYTES;
-    const int64_t kx = (int64_t)kt * BK;
+    const uint32_t kx = (uint32_t)kt * BK;
     const int lane_now = lane_opaque();
 #pragma unroll
     for (int j = 0; j < G::XPIECES; ++j) {
       const int row = 32 * wave + 16 * j + (lane_now >> 2);
       int gm = sr.m0 + row;
       gm = gm < M ? gm : M - 1;  // clamp the tail: staged, never stored
-      const int lg = ((lane_now & 3) ^ (((row >> 2) & 1) << 1)) * 16;
-      dma16(A + (int64_t)gm * lda + lg + kx, __builtin_amdgcn_readfirstlane(sx + (32 * wave + 16 * j) * BK));
+      const uint32_t lg = (uint32_t)(((lane_now & 3) ^ (((row >> 2) & 1) << 1)) * 16);
+      dma16s(A, (uint32_t)gm * (uint32_t)lda + lg + kx, __builtin_amdgcn_readfirstlane(sx + (32 * wave + 16 * j) * BK));
     }
-    const int8_t* wt = sr.w + (int64_t)kt * G::WBYTES + wave * (G::WPIECES * 1024) + lane_now * 16;
+    const uint32_t wt = sr.w + (uint32_t)kt * G::WBYTES + (uint32_t)(wave * (G::WPIECES * 1024) + lane_now * 16);
 #pragma unroll
     for (int j = 0; j < G::WPIECES; ++j)
-      dma16(wt + j * 1024, __builtin_amdgcn_readfirstlane(sw + (WROWS_PER_WAVE * wave + WROWS_PER_PIECE * j) * G::WROW));
+      dma16s(Wp, wt + j * 1024, __builtin_amdgcn_readfirstlane(sw + (WROWS_PER_WAVE * wave + WROWS_PER_PIECE * j) * G::WROW));
   };
 
-  // per-lane fragment offsets inside a stage
-  const int xoff = (128 * wm + fr) * BK + ((fq ^ (((fr >> 2) & 1) << 1)) << 4);
-  const int woff = (WFMT == QVIT_W4) ? (64 * wn + fr) * G::WROW + ((fq ^ (((fr >> 3) & 1) << 1)) << 3)
-                                     : (64 * wn + fr) * G::WROW + ((fq ^ (((fr >> 2) & 1) << 1)) << 4);
+  // per-lane fragment offsets inside a stage, recomputed from the lane id at each read (a few VALU per
+  // k-step) rather than held in registers across the register-bound main loop
   auto read_frags = [&](int rslot, Frags<WFMT>& f) {
+    const int ln = lane_opaque();
+    const int lfr = ln & 15, lfq = ln >> 4;
+    const int xoff = (128 * wm + lfr) * BK + ((lfq ^ (((lfr >> 2) & 1) << 1)) << 4);
+    const int woff = (WFMT == QVIT_W4) ? (64 * wn + lfr) * G::WROW + ((lfq ^ (((lfr >> 3) & 1) << 1)) << 3)
+                                       : (64 * wn + lfr) * G::WROW + ((lfq ^ (((lfr >> 2) & 1) << 1)) << 4);
     const int8_t* sx = smem + rslot * G::STAGE;
     const int8_t* sw = sx + XBYTES;
 #pragma unroll
@@ -540,6 +559,52 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
       if (has_bias) b4 = *reinterpret_cast<const float4*>(bias_l + (n - n0));
       float* Cf = reinterpret_cast<float*>(C);
       float4 old[2][4];
+      if (m0 + BM <= M && n0 + BN <= N) {
+        // whole tile: the residual rows are loaded by inline asm, which the compiler does not track,
+        // and waited for with exact counts (pass sr's loads are older than the previous pass's 4 stores
+        // and the next pass's 4 loads), so neither the loads of pass sr + 1 nor the stores in flight are
+        // drained at every pass, as the compiler's own vmcnt(0) would (the DMA ring is in flight)
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        f4v ov0[4], ov1[4];
+        auto ld = [&](int sr, f4v (&ov)[4]) __attribute__((always_inline)) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float* src = Cf + (int64_t)(m0 + 128 * wm + 16 * sr + 4 * i + prow) * ldc + n;
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(ov[i]) : "v"(src) : "memory");
+          }
+        };
+        auto pass = [&](int sr, f4v (&ov)[4]) __attribute__((always_inline)) {
+          __builtin_amdgcn_s_waitcnt(0xC07F);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            *reinterpret_cast<v4i*>(stg + efr * EPI_LD + 16 * efq + 4 * r) = acc[r][sr];
+          __builtin_amdgcn_s_waitcnt(0xC07F);
+          __builtin_amdgcn_wave_barrier();
+          // tie the wait to the loaded registers, so no use of them is scheduled above it
+          if (sr == 0 || sr == 7)
+            asm volatile("s_waitcnt vmcnt(4)" : "+v"(ov[0]), "+v"(ov[1]), "+v"(ov[2]), "+v"(ov[3]) :: "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(8)" : "+v"(ov[0]), "+v"(ov[1]), "+v"(ov[2]), "+v"(ov[3]) :: "memory");
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = 4 * i + prow;
+            const int m = m0 + 128 * wm + 16 * sr + row;
+            const v4i a4 = *reinterpret_cast<const v4i*>(stg + row * EPI_LD + pcol);
+            float4 o = make_float4(alpha * (float)a4[0] + b4.x, alpha * (float)a4[1] + b4.y,
+                                   alpha * (float)a4[2] + b4.z, alpha * (float)a4[3] + b4.w);
+            o.x += ov[i][0]; o.y += ov[i][1]; o.z += ov[i][2]; o.w += ov[i][3];
+            *reinterpret_cast<float4*>(Cf + (int64_t)m * ldc + n) = o;
+          }
+        };
+        ld(0, ov0);
+#pragma unroll
+        for (int sr = 0; sr < 8; sr += 2) {
+          ld(sr + 1, ov1);
+          pass(sr, ov0);
+          if (sr + 2 < 8) ld(sr + 2, ov0);
+          pass(sr + 1, ov1);
+        }
+      } else {
       auto load_old = [&](int sr, float4 (&ov)[4]) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -578,6 +643,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
             }
           }
         }
+      }
       }
     } else if (EPI == QVIT_EPI_QKV_SPLIT) {
       // fp16 hi/lo planes: 8 lanes per 64-column head-plane row, 8 columns (16 B of hi, 16 B of lo) each
@@ -735,15 +801,28 @@ int launch(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, i
   constexpr int WMV = 1;
 #endif
   using G = Geo<WFMT, WMV>;
-  const int64_t ntiles = (npad / BN) * ((M + G::BM - 1) / G::BM);
-  // resident blocks, a multiple of 8 (one team per XCD), no more than the tiles need
-  int64_t grid = (int64_t)device_cus() * G::MIN_BLOCKS / 8 * 8;
-  const int64_t need = (ntiles + 7) / 8 * 8;
-  if (grid > need) grid = need;
-  if (grid < 8) grid = 8;
-  hipLaunchKernelGGL((gemm_kernel<WFMT, EPI, WMV>), dim3((unsigned)grid), dim3(G::NT), 0, stream, A, (int)M, (int)K,
-                     lda, reinterpret_cast<const int8_t*>(Wp), (int)N, (int)npad, C, ldc, ep);
-  return qvit_hip_status(hipGetLastError());
+  // the kernel addresses A and Wp as 32-bit byte offsets from the base pointers: rows are launched in
+  // chunks whose A span stays below 2^32 (one chunk for every ViT / UltraNet shape)
+  const int64_t span = (int64_t)0xFFFFFFFF - K;
+  int64_t rows = span / lda / G::BM * G::BM;
+  if (rows < G::BM || npad * (K / (WFMT == QVIT_W4 ? 2 : 1)) > span) return QVIT_EINVAL;
+  if (EPI == QVIT_EPI_QKV_SPLIT && rows < M) return QVIT_EINVAL;  // its row -> (image, token) map is global
+  const int64_t esize = (EPI == QVIT_EPI_I8 || EPI == QVIT_EPI_I8_GELU) ? 1 : 4;
+  for (int64_t m0 = 0; m0 < M; m0 += rows) {
+    const int64_t mc = (M - m0 < rows) ? M - m0 : rows;
+    const int64_t ntiles = (npad / BN) * ((mc + G::BM - 1) / G::BM);
+    // resident blocks, a multiple of 8 (one team per XCD), no more than the tiles need
+    int64_t grid = (int64_t)device_cus() * G::MIN_BLOCKS / 8 * 8;
+    const int64_t need = (ntiles + 7) / 8 * 8;
+    if (grid > need) grid = need;
+    if (grid < 8) grid = 8;
+    void* Cc = reinterpret_cast<int8_t*>(C) + (EPI == QVIT_EPI_QKV_SPLIT ? 0 : m0 * ldc * esize);
+    hipLaunchKernelGGL((gemm_kernel<WFMT, EPI, WMV>), dim3((unsigned)grid), dim3(G::NT), 0, stream, A + m0 * lda,
+                       (int)mc, (int)K, lda, reinterpret_cast<const int8_t*>(Wp), (int)N, (int)npad, Cc, ldc, ep);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return qvit_hip_status(e);
+  }
+  return QVIT_OK;
 }
 
 template <int WFMT>

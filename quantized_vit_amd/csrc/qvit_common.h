@@ -146,7 +146,8 @@ struct EpiTableEnt {
 // fma itself rounds to the bucket index, which then sits in f's low mantissa bits: bits(f) = 0x4B000000 + j.
 // Monotone in v (the builder's bisection relies on it); one FMA and one med3, no float->int conversion,
 // and the entry's byte offset is one shift-add of bits(f).
-QVIT_DEV float epi_top(int nb) { return 8388608.f + (float)(nb - 1); }
+// 2^23 + nb - 1 from its bit pattern (integer add: stays on the scalar unit for a uniform nb)
+QVIT_DEV float epi_top(int nb) { return __int_as_float(0x4B000000 + nb - 1); }
 QVIT_DEV uint32_t epi_bucket_bits(float v, float C, float inv_w, float top) {
   return __float_as_uint(__builtin_amdgcn_fmed3f(fmaf(v, inv_w, C), 8388608.f, top));
 }
