@@ -70,8 +70,8 @@ def main():
     if a.stamps:
         assert lib.qvit_gemm_stamps(buf, 0) == 0
         waves = max(buf[7], 1)
-        names = ["head_wait", "dma_issue", "stage_wait", "reads+mfma", "epilogue", "tile_setup"]
-        per = [buf[i] / waves for i in range(6)]
+        names = ["head_wait", "dma_issue", "stage_wait", "reads+mfma", "epilogue", "tile_setup", "lgkm_wait"]
+        per = [buf[i] / waves for i in range(7)]
         tot = sum(per)
         print("per wave: " + "  ".join(f"{n} {v:8.0f} ({100*v/tot:4.1f}%)" for n, v in zip(names, per)))
     del vit_model, epilogue_table

@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 DIAG = os.path.join(ROOT, "tools", "_diag")
 LIB = os.path.join(DIAG, "libqvit_hip_stamps.so")
-PHASES = ["head_wait", "dma_issue", "stage_wait", "reads+mfma", "epilogue", "tile_setup"]
+PHASES = ["head_wait", "dma_issue", "stage_wait", "reads+mfma", "epilogue", "tile_setup", "lgkm_wait"]
 
 
 def main():
@@ -80,7 +80,7 @@ def main():
         torch.cuda.synchronize()
         assert lib.qvit_gemm_stamps(buf, 0) == 0
         waves = max(buf[7], 1)
-        per = [buf[i] / waves for i in range(6)]
+        per = [buf[i] / waves for i in range(7)]
         tot = sum(per)
         nk = K // 64
         tiles = ((N + 255) // 256) * ((M + 127) // 128)
