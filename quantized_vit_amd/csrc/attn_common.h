@@ -67,6 +67,10 @@ QVIT_DEV float xsum(float v) {
 
 // Diagnostic build only (-DQVIT_ATT_STAMPS, tools/attn_bench.py --stamps): per-phase s_memtime sums
 // (0 block wait + DMA issue, 1 scores, 2 softmax, 3 PV, 4 epilogue, 5 query-block reads).
+#ifndef QVIT_ATT_DEFER
+#define QVIT_ATT_DEFER 1
+#endif
+
 #ifdef QVIT_ATT_STAMPS
 static __device__ unsigned long long qvit_att_stamp_sums[16];
 struct Stamps {
@@ -101,7 +105,7 @@ struct Stamps {
 // s[i][kt][j] = S^T[key kbase + 16 kt + j][query of the lane]; scores in log2 units (sl2).
 // MASK: the block holds keys >= N (the last block only).
 // T: query tiles per wave (arrays); IMGS: byte distance between the K hi, K lo, V hi and V lo images.
-template <int T, int IMGS = IMG>
+template <int T, int IMGS = IMG, bool VEARLY = false>
 QVIT_DEV void attend(int nt, bool mask, const int8_t* st, const h8 (&qh)[T][2], const h8 (&ql)[T][2], float (&m)[T],
                      float (&l)[T], f4 (&o)[T][4], const int (&koffs)[2][2], const int (&voffs)[4], int kbase,
                      int N, float sl2, Stamps& sp) {
@@ -125,11 +129,26 @@ QVIT_DEV void attend(int nt, bool mask, const int8_t* st, const h8 (&qh)[T][2], 
       for (int kt = 0; kt < 2; ++kt) {
         s[i][kt] = f4{0.f, 0.f, 0.f, 0.f};
         if (i == NT - 1 && nt < NT) continue;  // wave-uniform: no 4th tile
+#if defined(QVIT_ATT_ABL) && QVIT_ATT_ABL == 4
+        s[i][kt] = f4{kh[kt][0][0], kl[kt][1][1], qh[i][0][0], ql[i][1][1]};  // diagnostic: no S MFMAs
+        continue;
+#endif
 #pragma unroll
         for (int c = 0; c < 2; ++c) s[i][kt] = mfma3(kh[kt][c], kl[kt][c], qh[i][c], ql[i][c], s[i][kt]);
       }
   }
   sp.mark(1);
+  // VEARLY: the V fragments of the whole block are issued before the softmax and land while it runs, so
+  // the P.V products never wait on an LDS round trip (read per 16-dim slice, each slice waits on one);
+  // it costs 32 registers, which the split kernel (4 query tiles per wave) does not have
+  h8 vh[4], vl[4];
+  if (VEARLY) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      vh[dt] = join(tr_read(st + 2 * IMGS, voffs[dt]), tr_read(st + 2 * IMGS, voffs[dt] + 16 * 128));
+      vl[dt] = join(tr_read(st + 3 * IMGS, voffs[dt]), tr_read(st + 3 * IMGS, voffs[dt] + 16 * 128));
+    }
+  }
   h8 ph[NT], pl[NT];
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
@@ -172,11 +191,17 @@ QVIT_DEV void attend(int nt, bool mask, const int8_t* st, const h8 (&qh)[T][2], 
   sp.mark(2);
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) {
-    const h8 vh = join(tr_read(st + 2 * IMGS, voffs[dt]), tr_read(st + 2 * IMGS, voffs[dt] + 16 * 128));
-    const h8 vl = join(tr_read(st + 3 * IMGS, voffs[dt]), tr_read(st + 3 * IMGS, voffs[dt] + 16 * 128));
+    if (!VEARLY) {
+      vh[dt] = join(tr_read(st + 2 * IMGS, voffs[dt]), tr_read(st + 2 * IMGS, voffs[dt] + 16 * 128));
+      vl[dt] = join(tr_read(st + 3 * IMGS, voffs[dt]), tr_read(st + 3 * IMGS, voffs[dt] + 16 * 128));
+    }
+#if defined(QVIT_ATT_ABL) && QVIT_ATT_ABL == 5
+    for (int i = 0; i < NT; ++i) o[i][dt] += f4{vh[dt][0], vl[dt][1], ph[i][2], pl[i][3]};  // diagnostic: no PV MFMAs
+    continue;
+#endif
 #pragma unroll
-    for (int i = 0; i < NT - 1; ++i) o[i][dt] = mfma3(vh, vl, ph[i], pl[i], o[i][dt]);
-    if (nt == NT) o[NT - 1][dt] = mfma3(vh, vl, ph[NT - 1], pl[NT - 1], o[NT - 1][dt]);
+    for (int i = 0; i < NT - 1; ++i) o[i][dt] = mfma3(vh[dt], vl[dt], ph[i], pl[i], o[i][dt]);
+    if (nt == NT) o[NT - 1][dt] = mfma3(vh[dt], vl[dt], ph[NT - 1], pl[NT - 1], o[NT - 1][dt]);
   }
   sp.mark(3);
 }

@@ -17,6 +17,7 @@
 #include "attn_common.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace {
 
@@ -31,6 +32,12 @@ constexpr int IMGF = IROWS * 128;         // 26 KiB per fp16 image
 constexpr int KV_BYTES = 4 * IMGF + 2048; // K hi, K lo, V hi, V lo + zero rows past V lo (last key block)
 constexpr int WSLOT = 3 * 4096;           // q, k, v 64-row weight groups of one k-step, unpacked to int8
 constexpr int WRING = 3;
+#ifndef QVIT_QA_SKIP
+#define QVIT_QA_SKIP 1
+#endif
+#ifndef QVIT_QA_PAIR
+#define QVIT_QA_PAIR 1
+#endif
 constexpr int TBL = 8192;                 // code table (<= 1022 buckets)
 constexpr int BIAS_MAX = 9216;            // fp32 bias of the qkv layer (<= 2304 features: H * 64 <= 768)
 constexpr int LDS_TOTAL = KV_BYTES + WRING * WSLOT + TBL + BIAS_MAX;
@@ -172,33 +179,66 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
     for (int tt = 0; tt < TPW; ++tt)
 #pragma unroll
       for (int f = 0; f < 12; ++f) acc[tt][f] = v4i{0, 0, 0, 0};
-    auto kstep = [&](int s, int q) __attribute__((always_inline)) {  // q = s % 4, compile-time after unrolling
+    // k-step s (ring slot q = s % 4, compile-time after unrolling). The two waves of a SIMD (w, w + 4)
+    // take opposite orders around the one barrier per k-step, so that one issues its MFMAs while the
+    // other issues its loads and weight staging: waves 0-3 compute first and stage the slot they fill
+    // (g + 1) after their MFMAs, waves 4-7 stage first. Either order writes slot g + 1 after barrier
+    // g - 1 (its last reader, step g - 2, is done) and before barrier g + 1 (its first read).
+    auto issue = [&](int s, int q) __attribute__((always_inline)) {
       if (s + 3 < nk) load_step(cur, s + 3, xa[(q + 3) & 3], wst[(q + 3) & 3]);
       else load_step(nxt, s + 3 - nk, xa[(q + 3) & 3], wst[(q + 3) & 3]);
       sp.mark(5);
       write_w(g + 1, wst[(q + 1) & 3]);
       sp.mark(6);
-      __syncthreads();
-      sp.mark(7);
+    };
+    // TWO: the wave's second token tile is inside the image (otherwise its MFMAs are skipped: 3 of the 16
+    // tiles of N = 197)
+    auto mma = [&](auto two, int q) __attribute__((always_inline)) {
       const int8_t* ws = wring + (g % WRING) * WSLOT;
       v4i wfr[12];
 #pragma unroll
       for (int f = 0; f < 12; ++f) wfr[f] = *reinterpret_cast<const v4i*>(ws + (f >> 2) * 4096 + woff + (f & 3) * 16 * 64);
+#if defined(QVIT_ATT_ABL) && QVIT_ATT_ABL == 6
+#pragma unroll
+      for (int f = 0; f < 12; ++f) acc[f & 1][f] ^= wfr[f] ^ xa[q][f & 1];  // diagnostic: no projection MFMAs
+      sp.mark(8);
+      return;
+#endif
 #pragma unroll
       for (int f = 0; f < 12; ++f) {
         const v4i wf = wfr[f];
         acc[0][f] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wf, xa[q][0], acc[0][f], 0, 0, 0);
-        acc[1][f] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wf, xa[q][1], acc[1][f], 0, 0, 0);  // tile may be past N
+        if (decltype(two)::value) acc[1][f] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wf, xa[q][1], acc[1][f], 0, 0, 0);
       }
       sp.mark(8);
+    };
+    auto kstep = [&](auto first, auto two, int s, int q) __attribute__((always_inline)) {
+      if (!decltype(first)::value) {
+        issue(s, q);
+        __syncthreads();
+        sp.mark(7);
+        mma(two, q);
+      } else {
+        __syncthreads();
+        sp.mark(7);
+        mma(two, q);
+        issue(s, q);
+      }
       ++g;
     };
-    for (int s = 0; s < nk; s += 4) {
-      kstep(s, 0);
-      kstep(s + 1, 1);
-      kstep(s + 2, 2);
-      kstep(s + 3, 3);
-    }
+    auto kloop = [&](auto first, auto two) __attribute__((always_inline)) {
+      for (int s = 0; s < nk; s += 4) {
+        kstep(first, two, s, 0);
+        kstep(first, two, s + 1, 1);
+        kstep(first, two, s + 2, 2);
+        kstep(first, two, s + 3, 3);
+      }
+    };
+    const bool first = QVIT_QA_PAIR && wave < 4;
+    if (first && (QVIT_QA_SKIP == 0 || tv[1])) kloop(std::true_type{}, std::true_type{});
+    else if (first) kloop(std::true_type{}, std::false_type{});
+    else if (QVIT_QA_SKIP == 0 || tv[1]) kloop(std::false_type{}, std::true_type{});
+    else kloop(std::false_type{}, std::false_type{});
     cur = nxt;
     unit_src(j + 2, nxt);
     sp.mark(9);
@@ -260,7 +300,7 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
     const int nkb = (N + KB - 1) / KB;
     if (nt > 0) {
       for (int kb = 0; kb < nkb; ++kb)
-        attend<TPW, IMGF>(nt, (kb + 1) * KB > N, kv + kb * KB * 128, qh, ql, m, l, o, koffs, voffs, kb * KB + 4 * fq,
+        attend<TPW, IMGF, true>(nt, (kb + 1) * KB > N, kv + kb * KB * 128, qh, ql, m, l, o, koffs, voffs, kb * KB + 4 * fq,
                           N, sl2, sp);
     }
     sp.mark(0);
