@@ -162,31 +162,40 @@ QVIT_DEV void attend(int nt, bool mask, const int8_t* st, const h8 (&qh)[T][2], 
       continue;
     }
 #endif
-    float bm = -INFINITY;
+    // raw scores of this lane's query; sl2 (> 0) goes into the exponent's fma: the max of the scaled
+    // scores is sl2 times the max of the raw ones (rounding is monotone)
+    float r[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      x[e] = s[i][e >> 2][e & 3] * sl2;
-    }
+    for (int e = 0; e < 8; ++e) r[e] = s[i][e >> 2][e & 3];
     if (mask) {  // wave-uniform: the last key block only
 #pragma unroll
-      for (int e = 0; e < 8; ++e) x[e] = (kbase + 16 * (e >> 2) + (e & 3) < N) ? x[e] : -INFINITY;
+      for (int e = 0; e < 8; ++e) r[e] = (kbase + 16 * (e >> 2) + (e & 3) < N) ? r[e] : -INFINITY;
     }
+    float bm = fmaxf(fmaxf(fmaxf(r[0], r[1]), fmaxf(r[2], r[3])), fmaxf(fmaxf(r[4], r[5]), fmaxf(r[6], r[7])));
+    bm = xmax(bm) * sl2;
+#if QVIT_ATT_DEFER
+    // deferred max: the running max moves only when some query's block max exceeds it by more than 8
+    // (log2 units), so P <= 2^8 (exact in the fp16 hi/lo split) and o, l are rescaled only then; a query
+    // whose max did not grow gets alpha = exp2(0) = 1 exactly
+    if (__builtin_amdgcn_ballot_w64(bm > m[i] + 8.f) != 0)
+#endif
+    {
+      const float mn = fmaxf(m[i], bm);
+      const float alpha = __builtin_amdgcn_exp2f(m[i] - mn);
+      l[i] *= alpha;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) bm = fmaxf(bm, x[e]);
-    bm = xmax(bm);
-    const float mn = fmaxf(m[i], bm);
-    const float alpha = __builtin_amdgcn_exp2f(m[i] - mn);
+      for (int dt = 0; dt < 4; ++dt) o[i][dt] = o[i][dt] * alpha;
+      m[i] = mn;
+    }
+    const float nm = -m[i];
     float ps = 0.f;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      x[e] = __builtin_amdgcn_exp2f(x[e] - mn);
+      x[e] = __builtin_amdgcn_exp2f(fmaf(r[e], sl2, nm));
       ps += x[e];
     }
-    l[i] = l[i] * alpha + ps;
-    m[i] = mn;
+    l[i] += ps;
     split8(x, ph[i], pl[i]);
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) o[i][dt] = o[i][dt] * alpha;
   }
   sp.mark(2);
 #pragma unroll

@@ -66,6 +66,29 @@ def test_attention_row_stride_and_peaked_softmax(dev):
     assert err <= 1e-5 * ref.abs().max().item(), err
 
 
+@pytest.mark.parametrize("slope", [0.04, 0.08, 0.15])
+def test_attention_running_max_rescale_branch(dev, slope):
+    """Logits that rise with the key index (slope per key, natural units) plus one late spike: the
+    online softmax's running max grows by less than the deferral threshold in some key blocks (kept) and
+    by more in others (rescale of o and l), at block positions fixed by the data. Full-tensor fp64 check."""
+    B, N, H = 2, 197, 2
+    g = torch.Generator().manual_seed(int(slope * 1000))
+    qkv = torch.randn(B * N, 3 * H * 64, generator=g) * 0.2
+    x = qkv.view(B, N, 3, H, 64)
+    u = torch.randn(64, generator=g)
+    u /= u.norm()
+    j = torch.arange(N, dtype=torch.float32)
+    x[:, :, 0] += 4.0 * u                                        # q . u = 4 for every query
+    x[:, :, 1] += (slope * j / (4.0 * 0.125))[None, :, None, None] * u   # logit of key j ~ slope * j
+    x[0, 170, 1, 0] += (12.0 / (4.0 * 0.125)) * u                # +12 at key 170 (block 5), image 0 head 0
+    x[1, 40, 1, 1] += (12.0 / (4.0 * 0.125)) * u                 # +12 at key 40 (block 1), image 1 head 1
+    ref = ref_attention(qkv, B, N, H, 64, 0.125)
+    out = run(dev, B, N, H, qkv, 0.125)
+    assert torch.isfinite(out).all()
+    err = (out.double() - ref).abs().max().item()
+    assert err <= 1e-5 * ref.abs().max().item(), err
+
+
 def test_attention_in_scale_large_inputs(dev):
     """|q|, |k|, |v| beyond the fp16 range: a power-of-two in_scale keeps the split exact."""
     B, N, H = 1, 100, 2
