@@ -301,8 +301,11 @@ QVIT_DEV float wave_sum_fast(float v) {
 // gamma/beta, the quantizer scalars and the code table (QVIT_EPI_I8 semantics, nullable) are read once
 // per workgroup. Same arithmetic as layernorm_quant_reg_kernel, row for row.
 constexpr int LN_TBL_BYTES = 16384;
+#ifndef QVIT_LN_MINW
+#define QVIT_LN_MINW 1
+#endif
 template <int NV>
-__global__ __launch_bounds__(kThreads) void layernorm_quant_persist_kernel(
+__global__ __launch_bounds__(kThreads, QVIT_LN_MINW) void layernorm_quant_persist_kernel(
     const float* __restrict__ x, int64_t rows, int64_t cols, int64_t ldx, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, int qtype, const float* d, const float* qm, const float* t,
     int levels, int8_t* __restrict__ codes, int64_t ldc, int64_t kpad, const int8_t* __restrict__ table) {
@@ -310,6 +313,18 @@ __global__ __launch_bounds__(kThreads) void layernorm_quant_persist_kernel(
   const QParams p = load_qparams(qtype, d, qm, t, levels);
   const int lane = threadIdx.x & 63;
   const int tid = threadIdx.x;
+  const int64_t nwaves = ((int64_t)gridDim.x * kThreads) >> 6;
+  int64_t r = (blockIdx.x * (int64_t)kThreads + tid) >> 6;
+  float4 v[NV];
+  auto load_row = [&](int64_t rr, float4 (&dst)[NV]) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int64_t c = 4 * (lane + 64 * i);
+      dst[i] = (rr < rows && c < cols) ? *reinterpret_cast<const float4*>(x + rr * ldx + c)
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  load_row(r, v);  // the first row is in flight while the table is staged
   const int8_t* ent = nullptr;
   float c0 = 0.f, inv_w = 0.f, top = 0.f;
   if (table != nullptr) {
@@ -331,18 +346,6 @@ __global__ __launch_bounds__(kThreads) void layernorm_quant_persist_kernel(
     gv[i] = (gamma && c < cols) ? *reinterpret_cast<const float4*>(gamma + c) : make_float4(1.f, 1.f, 1.f, 1.f);
     bv[i] = (beta && c < cols) ? *reinterpret_cast<const float4*>(beta + c) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  const int64_t nwaves = ((int64_t)gridDim.x * kThreads) >> 6;
-  int64_t r = (blockIdx.x * (int64_t)kThreads + tid) >> 6;
-  float4 v[NV];
-  auto load_row = [&](int64_t rr, float4 (&dst)[NV]) {
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int64_t c = 4 * (lane + 64 * i);
-      dst[i] = (rr < rows && c < cols) ? *reinterpret_cast<const float4*>(x + rr * ldx + c)
-                                       : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  };
-  load_row(r, v);
   for (; r < rows; r += nwaves) {
     float4 vn[NV];
     load_row(r + nwaves, vn);
@@ -551,7 +554,7 @@ int qvit_layernorm_quant_i8(const float* x, int64_t rows, int64_t cols, int64_t 
                    (!gamma || (((uintptr_t)gamma) & 15) == 0) && (!beta || (((uintptr_t)beta) & 15) == 0);
   const int nv = (int)((cols + 255) / 256);
   const dim3 grid((unsigned)((rows + 3) / 4));
-  if (reg && nv <= 4) {  // persistent: <= 8 workgroups per CU, the table read once per workgroup
+  if (reg && nv <= 4) {  // persistent: as many workgroups as are co-resident, the table read once per workgroup
     static const int cus = [] {
       int dev = 0, n = 0;
       if (hipGetDevice(&dev) != hipSuccess ||
@@ -559,11 +562,21 @@ int qvit_layernorm_quant_i8(const float* x, int64_t rows, int64_t cols, int64_t 
         n = 256;
       return n;
     }();
-    const int64_t pg = std::min<int64_t>((rows + 3) / 4, 8 * (int64_t)cus);
+    // workgroups per CU that are resident together (registers bound it: 5 at NV = 3); a grid past that
+    // leaves a second, partly filled round of workgroups behind the first
+    auto resident = [](const void* fn) {
+      int n = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kThreads, 0) != hipSuccess || n <= 0) n = 4;
+      return std::min(n, 8);
+    };
     const int8_t* tab = reinterpret_cast<const int8_t*>(code_table);
-#define QVIT_LN_P(NV)                                                                                          \
-  hipLaunchKernelGGL(layernorm_quant_persist_kernel<NV>, dim3((unsigned)pg), dim3(kThreads), 0, stream, x, rows, \
-                     cols, ldx, gamma, beta, eps, qtype, d_quant, q_m, t_quant, levels, codes, ldc, kpad, tab)
+#define QVIT_LN_P(NV)                                                                                               \
+  do {                                                                                                              \
+    static const int per_cu = resident(reinterpret_cast<const void*>(&layernorm_quant_persist_kernel<NV>));         \
+    const int64_t pg = std::min<int64_t>((rows + 3) / 4, (int64_t)per_cu * cus);                                    \
+    hipLaunchKernelGGL(layernorm_quant_persist_kernel<NV>, dim3((unsigned)pg), dim3(kThreads), 0, stream, x, rows, \
+                       cols, ldx, gamma, beta, eps, qtype, d_quant, q_m, t_quant, levels, codes, ldc, kpad, tab);   \
+  } while (0)
     if (nv <= 1) QVIT_LN_P(1);
     else if (nv <= 2) QVIT_LN_P(2);
     else if (nv <= 3) QVIT_LN_P(3);
