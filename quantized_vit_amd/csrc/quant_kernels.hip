@@ -309,7 +309,10 @@ __global__ __launch_bounds__(kThreads, QVIT_LN_MINW) void layernorm_quant_persis
     const float* __restrict__ x, int64_t rows, int64_t cols, int64_t ldx, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, int qtype, const float* d, const float* qm, const float* t,
     int levels, int8_t* __restrict__ codes, int64_t ldc, int64_t kpad, const int8_t* __restrict__ table) {
-  __shared__ __attribute__((aligned(16))) int8_t tl[LN_TBL_BYTES];
+  // code table, then gamma and beta as float4 rows (read per row from LDS: held in registers they would
+  // cost 8 NV VGPRs and a wave per SIMD of occupancy)
+  __shared__ __attribute__((aligned(16))) int8_t tl[LN_TBL_BYTES + 2 * 4096];
+  float4* gbl = reinterpret_cast<float4*>(tl + LN_TBL_BYTES);
   const QParams p = load_qparams(qtype, d, qm, t, levels);
   const int lane = threadIdx.x & 63;
   const int tid = threadIdx.x;
@@ -338,14 +341,12 @@ __global__ __launch_bounds__(kThreads, QVIT_LN_MINW) void layernorm_quant_persis
       top = epi_top(hd.nb);
     }
   }
-  __syncthreads();
-  float4 gv[NV], bv[NV];
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int64_t c = 4 * (lane + 64 * i);
-    gv[i] = (gamma && c < cols) ? *reinterpret_cast<const float4*>(gamma + c) : make_float4(1.f, 1.f, 1.f, 1.f);
-    bv[i] = (beta && c < cols) ? *reinterpret_cast<const float4*>(beta + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int k = tid; k < 64 * NV; k += kThreads) {
+    const int64_t c = 4 * k;
+    gbl[k] = (gamma && c < cols) ? *reinterpret_cast<const float4*>(gamma + c) : make_float4(1.f, 1.f, 1.f, 1.f);
+    gbl[256 + k] = (beta && c < cols) ? *reinterpret_cast<const float4*>(beta + c) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  __syncthreads();
   for (; r < rows; r += nwaves) {
     float4 vn[NV];
     load_row(r + nwaves, vn);
@@ -369,8 +370,9 @@ __global__ __launch_bounds__(kThreads, QVIT_LN_MINW) void layernorm_quant_persis
     for (int i = 0; i < NV; ++i) {
       const int64_t c = 4 * (lane + 64 * i);
       if (c < cols) {
-        const float y[4] = {(v[i].x - mean) * rstd * gv[i].x + bv[i].x, (v[i].y - mean) * rstd * gv[i].y + bv[i].y,
-                            (v[i].z - mean) * rstd * gv[i].z + bv[i].z, (v[i].w - mean) * rstd * gv[i].w + bv[i].w};
+        const float4 gv = gbl[lane + 64 * i], bv = gbl[256 + lane + 64 * i];
+        const float y[4] = {(v[i].x - mean) * rstd * gv.x + bv.x, (v[i].y - mean) * rstd * gv.y + bv.y,
+                            (v[i].z - mean) * rstd * gv.z + bv.z, (v[i].w - mean) * rstd * gv.w + bv.w};
         uint32_t word;
         if (ent != nullptr) {
           uint2 e[4];
