@@ -8,8 +8,9 @@ model_to_quantize_model swaps the same 50 layers (ViT-B/16).
 When every GEMM site is a QuantizeLinear / QuantizeConv2d on its integer path and the input is on
 a ROCm device, forward() runs the fused MI355X pipeline per block (one residual buffer, updated in
 place by the GEMM epilogues):
-    LayerNorm+act-quant -> qkv GEMM (fp32 out) -> attention (torch fp32, reference formula)
-    -> act-quant -> proj GEMM (+= residual) -> LayerNorm+act-quant -> fc1 GEMM with GELU and fc2's
+    LayerNorm+act-quant -> qkv projection + attention + proj's act-quant in one kernel
+    (qvit_qkv_attention, N <= 208; longer sequences: qkv GEMM to fp16 hi/lo head planes -> streaming
+    attention) -> proj GEMM (+= residual) -> LayerNorm+act-quant -> fc1 GEMM with GELU and fc2's
     act-quant fused (int8 codes out) -> fc2 GEMM (+= residual)
 Otherwise each module runs on its own (still the HIP kernels for every quantized layer).
 """
