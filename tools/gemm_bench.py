@@ -77,7 +77,10 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--shapes", default="qkv,proj,fc1,fc1_f32,fc1_i32,fc1_i8,fc2")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--lib", default="", help="time another build of the library (same-box A/B)")
     a = ap.parse_args()
+    if a.lib:
+        _lib.load(a.lib)
     dev = torch.device("cuda:0")
     _lib.load()
     res = []
