@@ -65,11 +65,13 @@ QVIT_DEV float xsum(float v) {
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
-// Diagnostic build only (-DQVIT_ATT_STAMPS, tools/attn_bench.py --stamps): per-phase s_memtime sums
-// (0 block wait + DMA issue, 1 scores, 2 softmax, 3 PV, 4 epilogue, 5 query-block reads).
+// Deferred running max in the online softmax (attend); 0: rescale at every key block (A/B builds).
 #ifndef QVIT_ATT_DEFER
 #define QVIT_ATT_DEFER 1
 #endif
+
+// Diagnostic build only (-DQVIT_ATT_STAMPS, tools/attn_bench.py --stamps): per-phase s_memtime sums
+// (0 block wait + DMA issue, 1 scores, 2 softmax, 3 PV, 4 epilogue, 5 query-block reads).
 
 #ifdef QVIT_ATT_STAMPS
 static __device__ unsigned long long qvit_att_stamp_sums[16];
