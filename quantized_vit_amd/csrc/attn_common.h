@@ -116,12 +116,15 @@ QVIT_DEV void attend(int nt, bool mask, const int8_t* st, const h8 (&qh)[T][2], 
 #endif
   constexpr int NT = T;
   f4 s[NT][2];
+  // the last block's second 16 keys all past N (N % 32 in 1..16): their scores are masked, skip them
+  const bool half = mask && (kbase & ~31) + 16 >= N;  // kbase = block start + 4 g, g < 4
   {
     h8 kh[2][2], kl[2][2];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
+        if (kt == 1 && half) continue;
         kh[kt][c] = lds_h8(st, koffs[kt][c]);
         kl[kt][c] = lds_h8(st + IMGS, koffs[kt][c]);
       }
@@ -131,6 +134,7 @@ QVIT_DEV void attend(int nt, bool mask, const int8_t* st, const h8 (&qh)[T][2], 
       for (int kt = 0; kt < 2; ++kt) {
         s[i][kt] = f4{0.f, 0.f, 0.f, 0.f};
         if (i == NT - 1 && nt < NT) continue;  // wave-uniform: no 4th tile
+        if (kt == 1 && half) continue;        // wave-uniform
 #if defined(QVIT_ATT_ABL) && QVIT_ATT_ABL == 4
         s[i][kt] = f4{kh[kt][0][0], kl[kt][1][1], qh[i][0][0], ql[i][1][1]};  // diagnostic: no S MFMAs
         continue;
