@@ -34,7 +34,11 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--lib", default="", help="time another build of the library (same-box A/B)")
     a = ap.parse_args()
+    if a.lib:
+        from quantized_vit_amd import _lib
+        _lib.load(a.lib)
     dev = torch.device("cuda:0")
     model = random_ultranet(seed=0, device=dev)
     x = synthetic_images_u8(a.batch, 416, seed=1, device=dev)
