@@ -47,7 +47,9 @@ QVIT_DEV uint32_t nib16_lo(uint32_t p) { return (p << 4) & 0xF0F0F0F0u; }
 QVIT_DEV uint32_t nib16_hi(uint32_t p) { return p & 0xF0F0F0F0u; }
 typedef int v4i __attribute__((ext_vector_type(4)));
 
-template <int OUT>
+// NKC: the number of 64-deep k-steps when fixed at compile time (12: K = 768, every ViT-B / ViT-L qkv),
+// which unrolls the projection loop completely; 0: K / 64 at run time
+template <int OUT, int NKC>
 __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
     const int8_t* __restrict__ A, int K, int64_t lda, const int8_t* __restrict__ Wp, int npad,
     const float* __restrict__ d_act, const float* __restrict__ d_wt, const float* __restrict__ bias, int B, int N,
@@ -63,7 +65,7 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
   const int C = H * 64;
-  const int nk = K / 64;
+  const int nk = NKC > 0 ? NKC : K / 64;
 
   // ---- per-workgroup setup: scalars, bias, code table, the zero rows past V lo -----------------------
   const float alpha = (*d_act) * (*d_wt);
@@ -226,12 +228,24 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
       }
       ++g;
     };
+    // with NKC the k-steps of a unit are straight-line code: a loop back-edge carrying the register ring's
+    // in-flight loads makes hipcc wait vmcnt(0) at the loop head, draining the prefetch every 4 k-steps
     auto kloop = [&](auto first, auto two) __attribute__((always_inline)) {
-      for (int s = 0; s < nk; s += 4) {
-        kstep(first, two, s, 0);
-        kstep(first, two, s + 1, 1);
-        kstep(first, two, s + 2, 2);
-        kstep(first, two, s + 3, 3);
+      if constexpr (NKC > 0) {
+#pragma unroll
+        for (int s = 0; s < NKC; s += 4) {
+          kstep(first, two, s, 0);
+          kstep(first, two, s + 1, 1);
+          kstep(first, two, s + 2, 2);
+          kstep(first, two, s + 3, 3);
+        }
+      } else {
+        for (int s = 0; s < nk; s += 4) {
+          kstep(first, two, s, 0);
+          kstep(first, two, s + 1, 1);
+          kstep(first, two, s + 2, 2);
+          kstep(first, two, s + 3, 3);
+        }
       }
     };
     const bool first = QVIT_QA_PAIR && wave < 4;
@@ -345,14 +359,18 @@ extern "C" int qvit_qkv_attention(const int8_t* A, int64_t B, int64_t N, int64_t
   const int64_t grid = std::max<int64_t>(8, (int64_t)cus / 8 * 8);  // one workgroup per CU, a multiple of 8
   const int8_t* w = reinterpret_cast<const int8_t*>(Wp);
   const int8_t* tab = reinterpret_cast<const int8_t*>(epi_table);
-  if (out_mode == QVIT_ATT_F32)
-    hipLaunchKernelGGL(qkv_attn_kernel<0>, dim3((unsigned)grid), dim3(FT), 0, stream, A, (int)K, lda, w, (int)npad,
-                       d_act, d_wt, bias, (int)B, (int)N, (int)H, scale, in_scale, out, ldo, out_qtype, out_d, out_qm,
-                       out_t, out_levels, nullptr);
-  else
-    hipLaunchKernelGGL(qkv_attn_kernel<1>, dim3((unsigned)grid), dim3(FT), 0, stream, A, (int)K, lda, w, (int)npad,
-                       d_act, d_wt, bias, (int)B, (int)N, (int)H, scale, in_scale, out, ldo, out_qtype, out_d, out_qm,
-                       out_t, out_levels, tab);
+#define QVIT_QA_LAUNCH(OUTV, NKV, TAB)                                                                          \
+  hipLaunchKernelGGL((qkv_attn_kernel<OUTV, NKV>), dim3((unsigned)grid), dim3(FT), 0, stream, A, (int)K, lda, w,    \
+                     (int)npad, d_act, d_wt, bias, (int)B, (int)N, (int)H, scale, in_scale, out, ldo, out_qtype,   \
+                     out_d, out_qm, out_t, out_levels, TAB)
+  if (out_mode == QVIT_ATT_F32) {
+    if (K == 768) QVIT_QA_LAUNCH(0, 12, nullptr);
+    else QVIT_QA_LAUNCH(0, 0, nullptr);
+  } else {
+    if (K == 768) QVIT_QA_LAUNCH(1, 12, tab);
+    else QVIT_QA_LAUNCH(1, 0, tab);
+  }
+#undef QVIT_QA_LAUNCH
   return qvit_hip_status(hipGetLastError());
 }
 
