@@ -84,7 +84,9 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
   }
   // in_scale is a power of two: (alpha acc + b) s == alpha s acc + b s exactly, so it is folded in here
   for (int k = tid; k < 3 * C; k += FT) bias_l[k] = bias ? bias[k] * in_scale : 0.f;
-  const float alpha_s = alpha * in_scale;
+  // the accumulators hold 16 acc (16x-scaled int4 operands): float(16 acc) = 16 float(acc) exactly (|16 acc| <
+  // 2^24), so the 1/16 rides in the scale instead of a shift per element — the same fp32 values
+  const float alpha_s = alpha * in_scale * 0.0625f;
   // K / V images start zeroed (rows a unit does not write are then always finite), plus the zero rows
   for (int k = tid; k < KV_BYTES / 16; k += FT) reinterpret_cast<uint4*>(kv)[k] = make_uint4(0, 0, 0, 0);
 
@@ -273,7 +275,7 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
           const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj)
-            x[4 * r + jj] = fmaf(alpha_s, (float)(acc[tt][4 * p + r][jj] >> 4), bb[jj]);
+            x[4 * r + jj] = fmaf(alpha_s, (float)acc[tt][4 * p + r][jj], bb[jj]);
         }
         h8 hi0, lo0, hi1, lo1;
         float xa0[8], xa1[8];
