@@ -2,18 +2,29 @@
 per GPU (BASELINE.json configs[1]; N > 1 = configs[2], batch-sharded with an RCCL all-gather of logits).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 256] [--no-cpu-baseline]
-    torchrun --nproc-per-node N bench.py --gpus N ...
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-A step = one forward of the quantized ViT-B/16 over one batch of synthetic 224x224 images already
-resident in HBM (+ the logits all-gather when N > 1). Rank 0 prints ONE JSON line.
+`python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment starts the N ranks itself
+(torch.distributed.run as a child process, before anything touches the GPU) and exits with its code.
+Under a launcher, WORLD_SIZE must equal --gpus.
 
-roofline: the dominant kernel is the fc1 GEMM (W4A8 contraction with the fused GELU + fc2
-activation-quantizer epilogue). achieved = 2*M*N*K int8 ops per launch / its mean duration measured
-with HIP events around every fc1 launch inside the timed region (events on the launch stream);
-peak = gfx950 dense int8 MFMA rate; traffic = HBM bytes per launch from rocprofv3 PMC counters
-(profiles/fc1_traffic.json, written by tools/profile_fc1.sh) or null.
+A step = one forward of the quantized ViT-B/16 over this rank's batch of synthetic 224x224 images
+already resident in HBM, plus the logits all-gather when N > 1 (distributed.ShardedInference).
+Rank 0 prints ONE JSON line; `value` = all ranks' images / the max over ranks of the timed region.
+
+roofline: the dominant GEMM, fc1 (W4A8 contraction with the fused GELU + fc2 activation-quantizer
+epilogue). achieved = 2*M*N*K int8 ops per launch / its mean duration measured with HIP events
+around every fc1 launch inside the timed region (events on the launch stream); peak = gfx950 dense
+int8 MFMA rate; traffic = HBM bytes per launch from rocprofv3 PMC counters (profiles/fc1_traffic.json,
+written by tools/profile_fc1.sh) or null. `kernels` gives the same event timing for every hot kernel
+of the block (fused qkv+attention, proj, fc2, LayerNorm) with its algorithmic work; `model_frac` is
+the whole forward's int8 GEMM ops / ms_per_step / peak.
 cpu_baseline: the CPU oracle's fp32 fake-quant forward (the reference's op sequence restated,
-oracle/quant_oracle.py) on a bounded sample of the same workload, rank 0 only, N = 1 only.
+oracle/quant_oracle.py) on a bounded sample of the same workload, rank 0 only, N = 1 only, with as
+many intra-op threads as this process may run on (affinity, capped by a cgroup CPU quota).
+
+QVIT_BENCH_DRYRUN=1 (tests only): gloo on the CPU, a stand-in per-image model instead of the ViT, so
+the launcher / sharding / timing / JSON plumbing is testable without a GPU.
 """
 from __future__ import annotations
 
@@ -21,6 +32,8 @@ import argparse
 import json
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,15 +43,18 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from quantized_vit_amd import _lib, build as qbuild, vit_model  # noqa: E402
-from quantized_vit_amd.calibrate import build_quantized_vit, synthetic_images  # noqa: E402
+from quantized_vit_amd.distributed import ShardedInference  # noqa: E402
 
 METRIC = "images/sec ViT-B/16 int4 @224 batch 256; % int8-MFMA roofline"
 # gfx950 dense int8 MFMA: 256 CU x 4 SIMD x (16*16*64*2 ops / 16 clk) x 2.4 GHz
 INT8_PEAK_TOPS = 256 * 4 * 2048 * 2.4e9 / 1e12
+# dense fp16 MFMA (v_mfma_f32_16x16x32_f16): half the int8 rate
+FP16_PEAK_TFLOPS = INT8_PEAK_TOPS / 2
+HBM_PEAK_GBS = 8000.0
+DRYRUN = os.environ.get("QVIT_BENCH_DRYRUN") == "1"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -50,57 +66,170 @@ def parse():
     ap.add_argument("--cpu-iters", type=int, default=3)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--lib", default="", help=argparse.SUPPRESS)  # diagnostic: A/B another build of the library
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args, argv) -> int:
+    """Starts `args.gpus` ranks of this script under torch.distributed.run (one process per GPU) as a
+    child process and returns its exit code. Called before any GPU call in this process."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def usable_cores() -> dict:
+    """CPUs this process may run on: the affinity mask, capped by a cgroup v2/v1 CPU quota."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(p)))
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                p = int(f.read())
+            if q > 0:
+                quota = max(1, q // p)
+        except (OSError, ValueError):
+            pass
+    use = min(aff, quota) if quota else aff
+    return {"threads": use, "affinity": aff, "cgroup_quota": quota, "cpu_count": os.cpu_count()}
+
+
+def cpu_model_name() -> str:
+    name = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return name
 
 
 def cpu_baseline(model, model_name: str, x_gpu_logits_fn, img_size: int, batch: int, iters: int):
     """Times the oracle's fp32 fake-quant forward on the host cores (bounded sample) and checks the
     GPU logits on the same images against it."""
     from oracle import quant_oracle as O
-    from quantized_vit_amd.calibrate import VIT_CONFIGS
+    from quantized_vit_amd.calibrate import VIT_CONFIGS, synthetic_images
     mc = VIT_CONFIGS[model_name]
     cfg = O.ViTConfig(img_size=mc["img_size"], patch_size=mc["patch_size"], embed_dim=mc["embed_dim"],
                       depth=mc["depth"], num_heads=mc["num_heads"])
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
     img = synthetic_images(batch, img_size, seed=12345)
-    torch.set_num_threads(max(1, torch.get_num_threads()))
-    with torch.no_grad():
-        ref = O.vit_forward(sd, cfg, img)  # warm-up (also the parity reference)
-        times = []
-        for _ in range(iters):
-            t0 = time.perf_counter()
-            O.vit_forward(sd, cfg, img)
-            times.append(time.perf_counter() - t0)
-        gpu = x_gpu_logits_fn(img)
+    cores = usable_cores()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(cores["threads"])
+    try:
+        with torch.no_grad():
+            ref = O.vit_forward(sd, cfg, img)  # warm-up (also the parity reference)
+            times = []
+            for _ in range(iters):
+                t0 = time.perf_counter()
+                O.vit_forward(sd, cfg, img)
+                times.append(time.perf_counter() - t0)
+            gpu = x_gpu_logits_fn(img)
+            # the same fp32 oracle against itself in fp64: quantizer rounding ties resolve differently
+            # and the flips compound over the blocks, so this is the floor any fp32 implementation sits at
+            ref64 = O.vit_forward({k: v.double() for k, v in sd.items()}, cfg, img.double())
+        used = torch.get_num_threads()
+    finally:
+        torch.set_num_threads(prev)
     times.sort()
     med = times[len(times) // 2]
     rel = ((gpu.double().cpu() - ref.double()).norm() / ref.double().norm()).item()
-    # the same fp32 oracle against itself in fp64: quantizer rounding ties resolve differently and the
-    # flips compound over the blocks, so this distance is the floor any fp32 implementation sits at
-    with torch.no_grad():
-        ref64 = O.vit_forward({k: v.double() for k, v in sd.items()}, cfg, img.double())
     floor = ((ref.double() - ref64).norm() / ref64.norm()).item()
-    cpu_model = platform.processor() or platform.machine()
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    cpu_model = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
     return {
-        "value": batch / med, "unit": "img/s", "cores": torch.get_num_threads(), "kind": "port",
+        "value": batch / med, "unit": "img/s", "cores": used, "kind": "port",
         "sample": f"oracle fp32 fake-quant {model_name} forward, batch {batch}, median of {iters} after 1 warm-up "
-                  f"({cpu_model})",
+                  f"({cpu_model_name()}; {used} intra-op threads = affinity {cores['affinity']}"
+                  f"{', cgroup quota ' + str(cores['cgroup_quota']) if cores['cgroup_quota'] else ''}"
+                  f", os.cpu_count() {cores['cpu_count']})",
     }, rel, floor
 
 
+def model_gemm_ops(model, B: int) -> float:
+    """Sum of 2*M*N*K over the forward's quantized GEMMs (patch embed, 4 per block, head)."""
+    pe = model.patch_embed
+    P = pe.num_patches
+    T = P + model.num_tokens
+    k_pe = pe.proj.in_channels * pe.proj.kernel_size[0] * pe.proj.kernel_size[1]
+    ops = 2.0 * B * P * pe.proj.out_channels * k_pe
+    for blk in model.blocks:
+        for lin in (blk.attn.qkv, blk.attn.proj, blk.mlp.fc1, blk.mlp.fc2):
+            ops += 2.0 * B * T * lin.out_features * lin.in_features
+    if hasattr(model.head, "in_features"):
+        ops += 2.0 * B * model.head.out_features * model.head.in_features
+    return ops
+
+
+def kernel_work(model, B: int) -> dict:
+    """Algorithmic work of one launch of each timed kernel."""
+    blk = model.blocks[0]
+    T = model.patch_embed.num_patches + model.num_tokens
+    M = B * T
+    C = blk.attn.qkv.in_features
+    H = blk.attn.num_heads
+    hid = blk.mlp.fc1.out_features
+
+    def gemm(lin):
+        return 2.0 * M * lin.out_features * lin.in_features
+    attn_flops = 4.0 * B * H * T * T * 64    # S = q k^T and O = P v, 2 flops per MAC
+    return {
+        "fc1": {"int8_ops": gemm(blk.mlp.fc1), "bytes": M * C + hid * C / 2 + M * hid},
+        "fc2": {"int8_ops": gemm(blk.mlp.fc2), "bytes": M * hid + C * hid / 2 + 2 * 4 * M * C},
+        "proj": {"int8_ops": gemm(blk.attn.proj), "bytes": M * C + C * C / 2 + 2 * 4 * M * C},
+        "qkv_attn": {"int8_ops": gemm(blk.attn.qkv), "fp32_attn_flops": attn_flops, "bytes": M * C + 3 * C * C / 2 + M * C},
+        "ln": {"bytes": 4 * M * C + M * C},
+    }
+
+
+def load_profile_json(name: str, model_name: str, B: int):
+    path = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            j = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if j.get("batch") != B or j.get("model") != model_name:
+        return None
+    return j
+
+
 def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    argv = sys.argv[1:]
+    args = parse(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args, argv))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch with "
+                         f"--nproc-per-node equal to --gpus (or without a launcher: python bench.py --gpus N)")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if DRYRUN:
+        return dryrun_main(args, world, rank)
+
+    from quantized_vit_amd import _lib, build as qbuild, vit_model
+    from quantized_vit_amd.calibrate import build_quantized_vit, synthetic_images
     if world > 1:
         dist.init_process_group("nccl", init_method="env://")
     torch.cuda.set_device(local_rank)
@@ -114,22 +243,21 @@ def main():
     img_size = {"vit_base_patch16_224": 224, "vit_large_patch16_384": 384, "vit_tiny_patch16_224": 224}[args.model]
     model = build_quantized_vit(args.model, seed=args.seed, device=dev)
     B = args.batch
-    x = synthetic_images(B, img_size, seed=1000 + rank, device=dev)
-    ncls = model.head.out_features
-    gathered = torch.empty((world * B, ncls), device=dev) if world > 1 else None
+    x = synthetic_images(B, img_size, seed=1000 + rank, device=dev)   # this rank's shard, made on-device
+    sharded = ShardedInference(model)
+    global_batch = world * B
 
     def step():
-        logits = model(x)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, logits)
-        return logits
+        return sharded.forward_shard(x, global_batch)
 
+    names = ("fc1", "fc2", "proj", "qkv_attn", "ln")
     with torch.no_grad():
         for _ in range(args.warmup):
-            step()
+            out = step()
         torch.cuda.synchronize()
-        # fc1 launch timing inside the timed region
-        vit_model.KERNEL_TIMING["fc1"] = []
+        assert out.shape == (global_batch, model.head.out_features), out.shape
+        for n in names:
+            vit_model.KERNEL_TIMING[n] = []
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -140,38 +268,54 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
-        ev = vit_model.KERNEL_TIMING.pop("fc1")
-    fc1_ms = sum(s.elapsed_time(e) for s, e in ev) / max(1, len(ev))
+        events = {n: vit_model.KERNEL_TIMING.pop(n) for n in names}
+    launch_ms = {n: (sum(s.elapsed_time(e) for s, e in ev) / len(ev)) if ev else None for n, ev in events.items()}
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
 
-    blk = model.blocks[0]
-    M = B * (model.patch_embed.num_patches + 1)
-    fc1 = blk.mlp.fc1
-    ops = 2.0 * M * fc1.out_features * fc1.in_features
+    work = kernel_work(model, B)
+    fc1_ms = launch_ms["fc1"]
+    ops = work["fc1"]["int8_ops"]
     achieved = ops / (fc1_ms * 1e-3) / 1e12
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "fc1_traffic.json")
-    if os.path.exists(tpath):
-        try:
-            with open(tpath) as f:
-                tj = json.load(f)
-            if tj.get("batch") == B and tj.get("model") == args.model:
-                traffic = tj.get("traffic_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
+    tj = load_profile_json("fc1_traffic.json", args.model, B)
+    traffic = tj.get("traffic_bytes_per_launch") if tj else None
+    pmc = load_profile_json("pmc_mfma.json", args.model, B)
+
+    kernels = {}
+    for n in names:
+        ms = launch_ms[n]
+        if ms is None:
+            continue
+        w = work[n]
+        k = {"launch_us": ms * 1e3, "launches_per_step": len(events[n]) / args.steps,
+             "hbm_GBs_algorithmic": w["bytes"] / (ms * 1e-3) / 1e9}
+        if "int8_ops" in w:
+            k["int8_TOPS"] = w["int8_ops"] / (ms * 1e-3) / 1e12
+            k["frac_int8_peak"] = k["int8_TOPS"] / INT8_PEAK_TOPS
+        if "fp32_attn_flops" in w:
+            # bound of the fused kernel: its int8 projection at the int8 peak plus the attention's
+            # fp32-equivalent flops as 3 fp16 MFMA passes (hi*hi + hi*lo + lo*hi) at the fp16 peak
+            bound_s = w["int8_ops"] / (INT8_PEAK_TOPS * 1e12) + 3 * w["fp32_attn_flops"] / (FP16_PEAK_TFLOPS * 1e12)
+            k["frac_of_mfma_bound"] = bound_s / (ms * 1e-3)
+        if n == "ln":
+            k["frac_hbm_peak"] = k["hbm_GBs_algorithmic"] / HBM_PEAK_GBS
+        if pmc and n in pmc.get("kernels", {}):
+            k["pmc"] = pmc["kernels"][n]
+        kernels[n] = k
+    total_ops = model_gemm_ops(model, B)
 
     result = {
         "metric": METRIC,
-        "value": world * B * args.steps / elapsed,
+        "value": global_batch * args.steps / elapsed,
         "unit": "img/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step": ms_per_step,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -180,13 +324,18 @@ def main():
                 "W4 (nonlinear quantizer, t=1) / A8 calibrated",
         "config": {"workload": f"{args.model} int4w/int8a forward, batch {B} per GPU"
                                + (", RCCL all-gather of logits" if world > 1 else ""),
-                   "model": args.model, "global_batch": world * B, "seq_len": model.patch_embed.num_patches + 1,
+                   "model": args.model, "global_batch": global_batch, "seq_len": model.patch_embed.num_patches + 1,
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma", "kernel": "fc1 gemm_kernel<W4, EPI_I8_GELU>",
                      "achieved": achieved, "peak": INT8_PEAK_TOPS, "unit": "TFLOP/s",
                      "frac": achieved / INT8_PEAK_TOPS, "traffic": traffic,
                      "ops_per_launch": ops, "launch_ms": fc1_ms,
-                     "note": "int8 ops (TOPS) counted as 2*M*N*K"},
+                     "mfma_util": (pmc or {}).get("kernels", {}).get("fc1", {}).get("mfma_busy_frac"),
+                     "note": "int8 ops (TOPS) counted as 2*M*N*K; mfma_util = SQ_VALU_MFMA_BUSY_CYCLES / "
+                             "(GRBM_GUI_ACTIVE x CUs) from profiles/pmc_mfma.json"},
+        "model_frac": {"int8_ops_per_step": total_ops, "achieved_TOPS": total_ops / (ms_per_step * 1e-3) / 1e12,
+                       "frac": total_ops / (ms_per_step * 1e-3) / 1e12 / INT8_PEAK_TOPS},
+        "kernels": kernels,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         def gpu_logits(img):
@@ -197,6 +346,42 @@ def main():
         result["parity_oracle_fp32_vs_fp64"] = floor
     if rank == 0:
         print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def dryrun_main(args, world: int, rank: int) -> None:
+    """QVIT_BENCH_DRYRUN=1: the same launcher / shard / gather / max-over-ranks timing on gloo + CPU with
+    a stand-in per-image model (tests/test_bench_launcher.py)."""
+    if world > 1:
+        dist.init_process_group("gloo", init_method="env://")
+    B = args.batch
+    g = torch.Generator().manual_seed(1000 + rank)
+    x = torch.rand(B, 3, 8, 8, generator=g)
+    w = torch.ones(3 * 8 * 8, 10)
+    sharded = ShardedInference(lambda im: im.flatten(1) @ w)
+    global_batch = world * B
+    for _ in range(args.warmup):
+        out = sharded.forward_shard(x, global_batch)
+    assert out.shape == (global_batch, 10), out.shape
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sharded.forward_shard(x, global_batch)
+    if world > 1:
+        dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": global_batch * args.steps / elapsed, "unit": "img/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+                          "vs_baseline": None, "dtype": "fp32", "data": "dry run (stand-in model, CPU, gloo)",
+                          "config": {"workload": "dry run", "global_batch": global_batch,
+                                     "parallelism": f"dp{world}"}}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -128,6 +128,24 @@ def load_reference_checkpoint(path: str, head_dim: int = 64, device: Optional[to
     return vit_from_state_dict(obj, head_dim=head_dim, device=device)
 
 
+def load_weight_codes(model: nn.Module, codes: Dict[str, torch.Tensor]) -> int:
+    """Binds precomputed integer weight codes to the model's quantized layers (QuantizeMixin.load_weight_codes):
+    `codes` maps a layer name ("blocks.0.mlp.fc1") or its state_dict-style key ("blocks.0.mlp.fc1.weight_codes")
+    to k with quantize_weight(W) == d_quant_wt * k (quant_layers.py:332-354), e.g. exported next to a
+    checkpoint by the reference's own host, so the device runs on exactly the reference's int4 weights.
+    Returns the number of layers bound; an unknown name is an error."""
+    from .quant_layers import QuantizeMixin
+    layers = {n: m for n, m in model.named_modules() if isinstance(m, QuantizeMixin)}
+    n = 0
+    for key, c in codes.items():
+        name = key[:-len(".weight_codes")] if key.endswith(".weight_codes") else key
+        if name not in layers:
+            raise KeyError(f"no quantized layer named {name!r}")
+        layers[name].load_weight_codes(c)
+        n += 1
+    return n
+
+
 # ---- UltraNet npz (torch_export.py:94-131) ------------------------------------------------------------
 
 def _ultra_param_modules(model: nn.Module) -> List[nn.Module]:

@@ -50,12 +50,22 @@ class ShardedInference:
         self.model = model
         self.group = group
 
+    def world_rank(self) -> Tuple[int, int]:
+        if not dist.is_initialized():
+            return 1, 0
+        return dist.get_world_size(self.group), dist.get_rank(self.group)
+
     @torch.no_grad()
     def __call__(self, global_images: torch.Tensor) -> torch.Tensor:
-        world = dist.get_world_size(self.group) if dist.is_initialized() else 1
-        rank = dist.get_rank(self.group) if dist.is_initialized() else 0
+        world, rank = self.world_rank()
         s, e = shard_bounds(global_images.shape[0], world, rank)
-        local = self.model(global_images[s:e])
+        return self.forward_shard(global_images[s:e], global_images.shape[0])
+
+    @torch.no_grad()
+    def forward_shard(self, local_images: torch.Tensor, global_batch: int) -> torch.Tensor:
+        """This rank's images (already resident on its device, e.g. generated there) -> all logits."""
+        world, _ = self.world_rank()
+        local = self.model(local_images)
         if world == 1:
             return local
-        return gather_logits(local, global_images.shape[0], self.group)
+        return gather_logits(local, global_batch, self.group)

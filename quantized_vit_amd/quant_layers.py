@@ -72,6 +72,16 @@ def _qtype_code(qt: QuantizationType) -> int:
 
 _warned_grad = False
 
+# Parity instrumentation (tests): when CODE_TRACE is a dict, every int8 activation-code operand handed to
+# a layer's contraction is recorded as CODE_TRACE[layer] = codes[:, :K] (a stream-ordered copy), so a
+# checker can compare each quantizer boundary of a full forward with the reference's.
+CODE_TRACE: Optional[dict] = None
+
+
+def trace_codes(layer, codes: torch.Tensor, k: int) -> None:
+    if CODE_TRACE is not None:
+        CODE_TRACE[layer] = codes[:, :k].detach().clone()
+
 
 def _warn_no_grad() -> None:
     global _warned_grad
@@ -160,6 +170,7 @@ class QuantizeMixin:
         self.weight_clip_val = weight_clip_val
         self.act_clip_val = act_clip_val
         self._qplan: Optional[QuantPlan] = None
+        self._weight_codes: Optional[Tuple[tuple, torch.Tensor]] = None
 
     # -- reference API: fake-quant fp32 tensors (quant_layers.py:332-381) -------------------
     def quantize_weight(self, weight: torch.Tensor) -> torch.Tensor:
@@ -207,6 +218,32 @@ class QuantizeMixin:
         """Drops the cached quantized weight. Needed only after editing parameters through
         `.data` (which bypasses the version counter the cache keys on)."""
         self._qplan = None
+
+    def load_weight_codes(self, codes: Optional[torch.Tensor]) -> None:
+        """Uses the given integer weight codes k (quantize_weight(W) == d_quant_wt * k, quant_layers.py:332-354)
+        instead of deriving them on the device — e.g. the codes the reference's own host computed, so that
+        both sides run on identical int4 weights. The codes stay bound to the current parameter versions:
+        editing any parameter drops them (the device derives the codes again). `None` unbinds them."""
+        if codes is None:
+            self._weight_codes = None
+        else:
+            c = torch.as_tensor(codes).detach()
+            if c.is_floating_point() and not torch.equal(c, c.round()):
+                raise ValueError("weight codes must be integers")
+            if tuple(c.shape) != tuple(self.weight.shape):
+                raise ValueError(f"weight codes of shape {tuple(c.shape)} for a weight of shape "
+                                 f"{tuple(self.weight.shape)}")
+            self._weight_codes = (self._plan_key(), c.reshape(c.shape[0], -1).to(torch.int16))
+        self._qplan = None
+
+    def _bound_weight_codes(self, key: tuple) -> Optional[torch.Tensor]:
+        wc = self._weight_codes
+        if wc is None:
+            return None
+        if (wc[0][0],) + wc[0][3:] != (key[0],) + key[3:]:   # type or a parameter changed since the load
+            self._weight_codes = None
+            return None
+        return wc[1]
 
     def _quant_param_tensors(self):
         names = ["weight", "bias", "d_quant_wt", "q_m_wt", "t_quant_wt", "d_quant_act", "q_m_act", "t_quant_act"]
@@ -264,11 +301,25 @@ class QuantizeMixin:
                          qm_act=qm_act, t_act=t_act)
         w32 = w2 if (w2.dtype == torch.float32 and w2.is_contiguous()) else w2.float().contiguous()
         act_ok = wa and abs(la) <= 127
+        codes = self._bound_weight_codes(key)
+        if codes is not None:
+            cmax = int(codes.abs().max().item()) if codes.numel() else 0
+            if cmax > abs(lw):
+                raise ValueError(f"{type(self).__name__}: loaded weight code {cmax} exceeds the quantizer's "
+                                 f"saturation level {lw}")
+            plan.extra["weight_codes"] = True
+            # packing integer values with the linear quantizer at d = 1 reproduces them exactly
+            w32 = codes.to(device=dev, dtype=torch.float32).contiguous()
+            qt_pack, d_pack = _lib.QT_LINEAR, torch.ones(1, device=dev)
+            qm_pack, t_pack = torch.full((1,), 1024.0, device=dev), None
+        else:
+            qt_pack, d_pack, qm_pack, t_pack = qt, d_wt, qm_wt, t_wt
+        plan.extra["w_codes_src"] = (w32, qt_pack, d_pack, qm_pack, t_pack)
         if act_ok and abs(lw) <= 127:
             overflow = torch.zeros(1, dtype=torch.int32, device=dev)
             for wfmt in ((_lib.W4, _lib.W8) if abs(lw) <= 7 else (_lib.W8,)):
                 overflow.zero_()
-                packed = _lib.pack_weight(w32, qt, d_wt, qm_wt, t_wt, wfmt, npad, kpad, overflow)
+                packed = _lib.pack_weight(w32, qt_pack, d_pack, qm_pack, t_pack, wfmt, npad, kpad, overflow)
                 if int(overflow.item()) == 0:
                     plan.packed, plan.wfmt, plan.int_path = packed, wfmt, True
                     break
@@ -279,10 +330,36 @@ class QuantizeMixin:
             plan.extra["out_bound"] = abs(s[3] * s[0]) * k * abs(la) * abs(lw) + s[-1]
         if wa:   # host copies of the activation quantizer's scalars (epilogue code tables of the producer)
             plan.extra["act_host"] = (qt, s[3], s[4], s[5] if t_act is not None else 1.0, la)
-        else:
-            wq = _lib.fake_quant_f32(self.weight.detach().float(), qt, d_wt, qm_wt, t_wt)
-            plan.w_fakequant = wq
+        if not plan.int_path:   # weight-only mode, or levels that fit neither int4 nor int8 (e.g. 16/32 bits)
+            plan.w_fakequant = self._fake_quant_weight(plan)
+        plan.extra.pop("w_codes_src")
         return plan
+
+    def _fake_quant_weight(self, plan: QuantPlan) -> torch.Tensor:
+        src = plan.extra.get("w_codes_src")
+        if src is not None and plan.extra.get("weight_codes"):
+            return (plan.d_wt * src[0]).view_as(self.weight)      # d_w * k, as quantize_weight returns it
+        return _lib.fake_quant_f32(self.weight.detach().float(), plan.qtype, plan.d_wt, plan.qm_wt, plan.t_wt)
+
+    def weight_codes(self) -> torch.Tensor:
+        """The integer weight codes the device path uses ([N, K] float32 on the device): the loaded ones
+        (load_weight_codes) or the device quantizer's."""
+        plan = self.quant_plan()
+        wc = self._bound_weight_codes(plan.key)
+        if wc is not None:
+            return wc.to(device=plan.device, dtype=torch.float32)
+        w = self._weight_2d().float().contiguous()
+        if abs(plan.level_wt) > 127:
+            return (_lib.fake_quant_f32(w, plan.qtype, plan.d_wt, plan.qm_wt, plan.t_wt) / plan.d_wt).round()
+        codes = torch.empty((w.shape[0], plan.kpad), dtype=torch.int8, device=plan.device)
+        _lib.quantize_act_i8(w, plan.qtype, plan.d_wt, plan.qm_wt, plan.t_wt, 0, codes, plan.kpad)
+        return codes[:, :w.shape[1]].float()
+
+    def w_fakequant(self, plan: QuantPlan) -> torch.Tensor:
+        """The reference's quantize_weight(W) (quant_layers.py:332-354), cached on the plan."""
+        if plan.w_fakequant is None:
+            plan.w_fakequant = self._fake_quant_weight(plan)
+        return plan.w_fakequant
 
     def _check_input(self, x: torch.Tensor) -> None:
         if not x.is_cuda:
@@ -438,13 +515,14 @@ class QuantizeLinear(nn.Linear, QuantizeMixin):
             if x2.dtype != torch.float32 or x2.stride(-1) != 1:
                 x2 = x2.float().contiguous()
             codes = self._act_codes(x2, plan)
+            trace_codes(self, codes, plan.k)
             out = self.gemm_codes(codes, plan, _lib.EPI_F32)
             if out.shape[1] != plan.n:
                 out = out[:, :plan.n].contiguous()
             return out.view(*input_.shape[:-1], plan.n)
         x = self.quantize_act(input_.float()) if self.quant_mode == QuantizationMode.WEIGHT_AND_ACTIVATION \
             else input_.float()
-        return F.linear(x.detach(), plan.w_fakequant, None if self.bias is None else self.bias.detach())
+        return F.linear(x.detach(), self.w_fakequant(plan), None if self.bias is None else self.bias.detach())
 
 
 class QuantizeConv2d(nn.Conv2d, QuantizeMixin):
@@ -493,6 +571,7 @@ class QuantizeConv2d(nn.Conv2d, QuantizeMixin):
         codes = torch.empty((B * OH * OW, plan.kpad), dtype=torch.int8, device=x.device)
         _lib.im2col_quant_i8(x, kh, kw, sh, sw, ph, pw, dh, dw, plan.qtype, plan.d_act, plan.qm_act, plan.t_act, 0,
                              codes, plan.kpad)
+        trace_codes(self, codes, plan.k)
         out = self.gemm_codes(codes, plan, epilogue)
         return out, (B, OH, OW)
 
@@ -505,7 +584,7 @@ class QuantizeConv2d(nn.Conv2d, QuantizeMixin):
             return out[:, :n].reshape(B, OH, OW, n).permute(0, 3, 1, 2).contiguous()
         x = self.quantize_act(input_.float()) if self.quant_mode == QuantizationMode.WEIGHT_AND_ACTIVATION \
             else input_.float()
-        w = plan.w_fakequant.view_as(self.weight)
+        w = self.w_fakequant(plan).view_as(self.weight)
         return F.conv2d(x.detach(), w, None if self.bias is None else self.bias.detach(), self.stride,
                         self.padding, self.dilation, self.groups)
 

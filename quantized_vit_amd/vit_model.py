@@ -27,11 +27,30 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
-from .quant_layers import QuantizationMode, QuantizeConv2d, QuantizeLinear, epilogue_table
+from .quant_layers import QuantizationMode, QuantizeConv2d, QuantizeLinear, epilogue_table, trace_codes
 
-# Benchmark instrumentation: when KERNEL_TIMING["fc1"] is a list, the fused block appends a
-# (start, end) HIP event pair recorded on the launch stream around every fc1 GEMM launch.
+# Benchmark instrumentation: when KERNEL_TIMING[name] is a list (name in "fc1", "fc2", "proj",
+# "qkv_attn", "ln"), the fused block appends a (start, end) HIP event pair recorded on the launch
+# stream (torch's current stream, which every _lib entry point launches on) around each such launch.
 KERNEL_TIMING: dict = {}
+
+
+class _timed:
+    __slots__ = ("ev", "e0")
+
+    def __init__(self, name: str):
+        self.ev = KERNEL_TIMING.get(name)
+
+    def __enter__(self):
+        if self.ev is not None:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e0.record()
+
+    def __exit__(self, *exc):
+        if self.ev is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self.ev.append((self.e0, e1))
 
 
 def drop_path(x, drop_prob: float = 0., training: bool = False):
@@ -225,9 +244,11 @@ class Block(nn.Module):
         # x + attn(norm1(x))
         p_qkv = a.qkv.quant_plan()
         codes = torch.empty((M, p_qkv.kpad), dtype=torch.int8, device=x.device)
-        _lib.layernorm_quant_i8(x2, self.norm1.weight, self.norm1.bias, self.norm1.eps, p_qkv.qtype, p_qkv.d_act,
-                                p_qkv.qm_act, p_qkv.t_act, 0, codes, p_qkv.kpad,
-                                code_table=epilogue_table(p_qkv, _lib.EPI_I8))
+        with _timed("ln"):
+            _lib.layernorm_quant_i8(x2, self.norm1.weight, self.norm1.bias, self.norm1.eps, p_qkv.qtype,
+                                    p_qkv.d_act, p_qkv.qm_act, p_qkv.t_act, 0, codes, p_qkv.kpad,
+                                    code_table=epilogue_table(p_qkv, _lib.EPI_I8))
+        trace_codes(a.qkv, codes, C)
         p_proj = a.proj.quant_plan()
         if (a.split_ok(p_qkv) and N <= _lib.QKV_ATT_MAX_N and p_qkv.wfmt == _lib.W4 and p_qkv.kpad <= 65536
                 and p_qkv.kpad % 256 == 0 and a.num_heads * 64 <= _lib.QKV_ATT_MAX_C):
@@ -235,11 +256,14 @@ class Block(nn.Module):
             out = torch.empty((M, p_proj.kpad), dtype=torch.int8, device=x.device)
             if p_proj.kpad != a.num_heads * 64:
                 out[:, a.num_heads * 64:].zero_()
-            _lib.qkv_attention(codes, B, N, p_qkv.kpad, p_qkv.packed, p_qkv.npad, p_qkv.d_act, p_qkv.d_wt,
-                               p_qkv.bias_pad, a.num_heads, a.scale, out, _lib.ATT_I8, attention_in_scale(p_qkv),
-                               p_proj.qtype, p_proj.d_act, p_proj.qm_act, p_proj.t_act,
-                               epi_table=epilogue_table(p_proj, _lib.EPI_I8))
-            a.proj.gemm_codes(out, p_proj, _lib.EPI_F32_RESID, out=x2)
+            in_scale, tab = attention_in_scale(p_qkv), epilogue_table(p_proj, _lib.EPI_I8)
+            with _timed("qkv_attn"):
+                _lib.qkv_attention(codes, B, N, p_qkv.kpad, p_qkv.packed, p_qkv.npad, p_qkv.d_act, p_qkv.d_wt,
+                                   p_qkv.bias_pad, a.num_heads, a.scale, out, _lib.ATT_I8, in_scale,
+                                   p_proj.qtype, p_proj.d_act, p_proj.qm_act, p_proj.t_act, epi_table=tab)
+            trace_codes(a.proj, out, p_proj.k)
+            with _timed("proj"):
+                a.proj.gemm_codes(out, p_proj, _lib.EPI_F32_RESID, out=x2)
             return self._mlp_fused_(x, x2, M)
         if a.split_ok(p_qkv):
             # qkv as pre-scaled fp16 hi/lo head planes, then attention + proj's activation quantizer
@@ -254,6 +278,7 @@ class Block(nn.Module):
             _lib.attention_split(hi, lo, B, N, a.num_heads, 64, a.scale, codes, _lib.ATT_I8, in_scale,
                                  p_proj.qtype, p_proj.d_act, p_proj.qm_act, p_proj.t_act,
                                  epi_table=epilogue_table(p_proj, _lib.EPI_I8))
+            trace_codes(a.proj, codes, p_proj.k)
             a.proj.gemm_codes(codes, p_proj, _lib.EPI_F32_RESID, out=x2)
             return self._mlp_fused_(x, x2, M)
         qkv = a.qkv.gemm_codes(codes, p_qkv, _lib.EPI_F32)
@@ -268,6 +293,7 @@ class Block(nn.Module):
         else:
             h = a.core(qkv, B, N).reshape(M, -1)
             codes = a.proj._act_codes(h if h.is_contiguous() else h.contiguous(), p_proj)
+        trace_codes(a.proj, codes, p_proj.k)
         a.proj.gemm_codes(codes, p_proj, _lib.EPI_F32_RESID, out=x2)
         return self._mlp_fused_(x, x2, M)
 
@@ -276,22 +302,20 @@ class Block(nn.Module):
         m = self.mlp
         p_fc1 = m.fc1.quant_plan()
         codes = torch.empty((M, p_fc1.kpad), dtype=torch.int8, device=x.device)
-        _lib.layernorm_quant_i8(x2, self.norm2.weight, self.norm2.bias, self.norm2.eps, p_fc1.qtype, p_fc1.d_act,
-                                p_fc1.qm_act, p_fc1.t_act, 0, codes, p_fc1.kpad,
-                                code_table=epilogue_table(p_fc1, _lib.EPI_I8))
+        with _timed("ln"):
+            _lib.layernorm_quant_i8(x2, self.norm2.weight, self.norm2.bias, self.norm2.eps, p_fc1.qtype,
+                                    p_fc1.d_act, p_fc1.qm_act, p_fc1.t_act, 0, codes, p_fc1.kpad,
+                                    code_table=epilogue_table(p_fc1, _lib.EPI_I8))
+        trace_codes(m.fc1, codes, p_fc1.k)
         p_fc2 = m.fc2.quant_plan()
         hid = torch.empty((M, p_fc2.kpad), dtype=torch.int8, device=x.device)
         if p_fc2.kpad != p_fc1.n:
             hid[:, p_fc1.n:].zero_()
-        ev = KERNEL_TIMING.get("fc1")
-        if ev is not None:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-        m.fc1.gemm_codes(codes, p_fc1, _lib.EPI_I8_GELU, out=hid, next_layer=m.fc2)
-        if ev is not None:
-            e1.record()
-            ev.append((e0, e1))
-        m.fc2.gemm_codes(hid, p_fc2, _lib.EPI_F32_RESID, out=x2)
+        with _timed("fc1"):
+            m.fc1.gemm_codes(codes, p_fc1, _lib.EPI_I8_GELU, out=hid, next_layer=m.fc2)
+        trace_codes(m.fc2, hid, p_fc2.k)
+        with _timed("fc2"):
+            m.fc2.gemm_codes(hid, p_fc2, _lib.EPI_F32_RESID, out=x2)
         return x
 
     def forward(self, x):
