@@ -50,9 +50,6 @@ QVIT_DEV f4 mfma3(h8 ah, h8 al, h8 bh, h8 bl, f4 c) {
 // Cross-lane max / sum over the 4 lane groups g (xor 16, xor 32) with the gfx950 permlane swaps (VALU,
 // no LDS round trip); the sums add in the same order as a butterfly of shuffles.
 QVIT_DEV float xmax(float v) {
-#if defined(QVIT_ATT_ABL) && QVIT_ATT_ABL == 3
-  return v;  // diagnostic: no cross-lane step
-#endif
   const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
   const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
@@ -111,9 +108,6 @@ template <int T, int IMGS = IMG, bool VEARLY = false>
 QVIT_DEV void attend(int nt, bool mask, const int8_t* st, const h8 (&qh)[T][2], const h8 (&ql)[T][2], float (&m)[T],
                      float (&l)[T], f4 (&o)[T][4], const int (&koffs)[2][2], const int (&voffs)[4], int kbase,
                      int N, float sl2, Stamps& sp) {
-#if defined(QVIT_ATT_ABL) && QVIT_ATT_ABL == 1
-  return;  // diagnostic: operand streaming only
-#endif
   constexpr int NT = T;
   f4 s[NT][2];
   // the last block's second 16 keys all past N (N % 32 in 1..16): their scores are masked, skip them
@@ -135,10 +129,6 @@ QVIT_DEV void attend(int nt, bool mask, const int8_t* st, const h8 (&qh)[T][2], 
         s[i][kt] = f4{0.f, 0.f, 0.f, 0.f};
         if (i == NT - 1 && nt < NT) continue;  // wave-uniform: no 4th tile
         if (kt == 1 && half) continue;        // wave-uniform
-#if defined(QVIT_ATT_ABL) && QVIT_ATT_ABL == 4
-        s[i][kt] = f4{kh[kt][0][0], kl[kt][1][1], qh[i][0][0], ql[i][1][1]};  // diagnostic: no S MFMAs
-        continue;
-#endif
 #pragma unroll
         for (int c = 0; c < 2; ++c) s[i][kt] = mfma3(kh[kt][c], kl[kt][c], qh[i][c], ql[i][c], s[i][kt]);
       }
@@ -160,14 +150,6 @@ QVIT_DEV void attend(int nt, bool mask, const int8_t* st, const h8 (&qh)[T][2], 
   for (int i = 0; i < NT; ++i) {
     if (i == NT - 1 && nt < NT) continue;
     float x[8];
-#if defined(QVIT_ATT_ABL) && QVIT_ATT_ABL == 2
-    {  // diagnostic: MFMAs only (P = raw scores)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) x[e] = s[i][e >> 2][e & 3];
-      split8(x, ph[i], pl[i]);
-      continue;
-    }
-#endif
     // raw scores of this lane's query; sl2 (> 0) goes into the exponent's fma: the max of the scaled
     // scores is sl2 times the max of the raw ones (rounding is monotone)
     float r[8];
@@ -210,10 +192,6 @@ QVIT_DEV void attend(int nt, bool mask, const int8_t* st, const h8 (&qh)[T][2], 
       vh[dt] = join(tr_read(st + 2 * IMGS, voffs[dt]), tr_read(st + 2 * IMGS, voffs[dt] + 16 * 128));
       vl[dt] = join(tr_read(st + 3 * IMGS, voffs[dt]), tr_read(st + 3 * IMGS, voffs[dt] + 16 * 128));
     }
-#if defined(QVIT_ATT_ABL) && QVIT_ATT_ABL == 5
-    for (int i = 0; i < NT; ++i) o[i][dt] += f4{vh[dt][0], vl[dt][1], ph[i][2], pl[i][3]};  // diagnostic: no PV MFMAs
-    continue;
-#endif
 #pragma unroll
     for (int i = 0; i < NT - 1; ++i) o[i][dt] = mfma3(vh[dt], vl[dt], ph[i], pl[i], o[i][dt]);
     if (nt == NT) o[NT - 1][dt] = mfma3(vh[dt], vl[dt], ph[NT - 1], pl[NT - 1], o[NT - 1][dt]);

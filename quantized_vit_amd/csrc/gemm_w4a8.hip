@@ -121,12 +121,6 @@ QVIT_DEV void dma16s(const void* sbase, uint32_t voff, uint32_t lds_base) {
 template <int N>
 QVIT_DEV void stage_sync() {
   __builtin_amdgcn_s_waitcnt(0xC07F);
-#if defined(QVIT_GEMM_ABL)
-  if (QVIT_GEMM_ABL == 8) {  // diagnostic: no barrier (valid only with a static LDS image)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-    return;
-  }
-#endif
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
@@ -336,9 +330,6 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   };
   const uint32_t lds0 = lds_addr(smem);
   auto issue = [&](const Src& sr, int kt, int rslot) {
-#if defined(QVIT_GEMM_ABL)
-    if (QVIT_GEMM_ABL == 1) return;  // diagnostic: no DMA
-#endif
     const uint32_t sx = lds0 + (uint32_t)(rslot * G::STAGE);
     const uint32_t sw = sx + XBYTES;
     const uint32_t kx = (uint32_t)kt * BK;
@@ -483,16 +474,6 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc[r][sr][j] >>= 4;
     }
-#if defined(QVIT_GEMM_ABL)
-    if (QVIT_GEMM_ABL == 6) {  // diagnostic: no epilogue (accumulators folded into one store per lane)
-      int x = 0;
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int sr = 0; sr < 8; ++sr) x ^= acc[r][sr][0] ^ acc[r][sr][1] ^ acc[r][sr][2] ^ acc[r][sr][3];
-      if (x == 0x7fffffff) reinterpret_cast<int*>(C)[tid] = x;
-    } else
-#endif
     {
     // ---- epilogue (epilogue LDS region only; the next tile's DMA streams underneath) -----------
     // acc[r][s][j] = C[m0 + 128 wm + 16 s + fr][n0 + 64 wn + 16 fq + 4 r + j] (weight rows pre-permuted)

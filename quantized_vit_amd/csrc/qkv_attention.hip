@@ -47,8 +47,9 @@ QVIT_DEV uint32_t nib16_lo(uint32_t p) { return (p << 4) & 0xF0F0F0F0u; }
 QVIT_DEV uint32_t nib16_hi(uint32_t p) { return p & 0xF0F0F0F0u; }
 typedef int v4i __attribute__((ext_vector_type(4)));
 
-// NKC: the number of 64-deep k-steps when fixed at compile time (12: K = 768, every ViT-B / ViT-L qkv),
-// which unrolls the projection loop completely; 0: K / 64 at run time
+// NKC: the number of 64-deep k-steps when fixed at compile time (12: K = 768, the ViT-B qkv; ViT-L's
+// H * 64 = 1024 exceeds QKV_ATT_MAX_C and takes the split path), which unrolls the projection loop
+// completely; 0: K / 64 at run time (other K, e.g. 512 or 1024 with <= 12 heads)
 template <int OUT, int NKC>
 __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
     const int8_t* __restrict__ A, int K, int64_t lda, const int8_t* __restrict__ Wp, int npad,
@@ -202,12 +203,6 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
       v4i wfr[12];
 #pragma unroll
       for (int f = 0; f < 12; ++f) wfr[f] = *reinterpret_cast<const v4i*>(ws + (f >> 2) * 4096 + woff + (f & 3) * 16 * 64);
-#if defined(QVIT_ATT_ABL) && QVIT_ATT_ABL == 6
-#pragma unroll
-      for (int f = 0; f < 12; ++f) acc[f & 1][f] ^= wfr[f] ^ xa[q][f & 1];  // diagnostic: no projection MFMAs
-      sp.mark(8);
-      return;
-#endif
 #pragma unroll
       for (int f = 0; f < 12; ++f) {
         const v4i wf = wfr[f];

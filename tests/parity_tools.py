@@ -1,149 +1,3 @@
-"""Parity helpers shared by the GPU model tests (test infrastructure; imports the oracle as the checker).
-
-Tie-resolved comparison. The reference's quantizers are discontinuous: a pre-quantization value that
-lands within rounding noise of a code boundary ((k + 1/2) * d in the |x|^t domain) takes either code
-depending on ulp-level arithmetic — the fp32 reference differs from itself in fp64 this way, and torch's
-CPU exp/log (MKL VML, not correctly rounded) resolve such ties differently from any
-other implementation. One flipped code then moves everything downstream, and over 12 ViT-B blocks the
-flips compound to ~4e-2 of the logits.
-
-So the end-to-end check runs the oracle with every quantizer boundary of the GPU forward laid beside it:
-where the GPU's code differs from the oracle's own, the difference must be one code step AND the oracle's
-pre-quantization value must sit within TIE_TOL code units of the boundary between the two codes (a proven
-tie); the oracle then adopts the GPU's code and continues. Any other difference is a failure. With the ties
-resolved alike, the two forwards follow the same code trajectory and the logits must agree to fp32
-rounding (the north star's 1e-3, met with a wide margin).
-"""
-from __future__ import annotations
-
-from typing import Dict
-
-import torch
-
-from oracle import quant_oracle as O
-
-# |p(|x|)/d - (k + 1/2)| bound, in code units, for a difference to count as a rounding tie. The
-# pre-quantization values of the two implementations differ by ~1e-6 of a row's scale (LayerNorm,
-# fp32 epilogues, 22-bit attention operands), i.e. ~1e-4 code units at 127 levels.
-TIE_TOL = 4e-3
-
-
-def code_position(x: torch.Tensor, q_type: str, d: float, t: float) -> torch.Tensor:
-    """p(|x|) / d in fp64: the quantizer's rounding argument (code units)."""
-    ax = x.double().abs()
-    p = ax if q_type in (O.LINEAR, O.DGE) else torch.where(ax > 0, torch.exp(t * torch.log(ax)), torch.zeros_like(ax))
-    return p / d
-
-
-def tie_check(x: torch.Tensor, got: torch.Tensor, own: torch.Tensor, q_type: str, d: float, q_m: float,
-              t: float) -> dict:
-    """Compares codes `got` with the reference's own codes `own` of the values `x` (same shapes).
-    Returns counts: flips (differing codes), non_ties (differences that are not one-step rounding
-    ties), max_dist (largest tie distance from its boundary, code units)."""
-    got = got.reshape(own.shape).to(own.dtype)
-    diff = (got - own)
-    idx = diff != 0
-    n = int(idx.sum())
-    out = {"flips": n, "non_ties": 0, "max_dist": 0.0, "total": own.numel()}
-    if n == 0:
-        return out
-    xs, g, o = x.reshape(own.shape)[idx], got[idx], own[idx]
-    one_step = (g - o).abs() == 1
-    same_side = (g * o) >= 0                      # no sign change, except through 0
-    kmin = torch.minimum(g.abs(), o.abs()).double()
-    pos = code_position(xs, q_type, d, t)
-    dist = (pos - (kmin + 0.5)).abs()
-    # |x| at q_m switches to the saturation branch: treat the immediate neighbourhood of q_m as a tie too
-    near_qm = (xs.double().abs() - abs(q_m)).abs() <= 1e-5 * abs(q_m)
-    tie = one_step & same_side & ((dist <= TIE_TOL) | near_qm)
-    out["non_ties"] = int((~tie).sum())
-    out["max_dist"] = float(dist[tie & ~near_qm].max()) if bool((tie & ~near_qm).any()) else 0.0
-    return out
-
-
-def oracle_weight_codes(sd: Dict[str, torch.Tensor], prefix: str, q_type: str, q_mode: str) -> torch.Tensor:
-    """The reference's quantize_weight(W) / d_w as integers (quant_layers.py:332-354), on the CPU."""
-    q = O.LayerQ.from_state(sd, prefix + ".", q_type, q_mode)
-    return O.quant_codes(sd[prefix + ".weight"], q_type, q.d_wt, q.q_m_wt, q.t_wt).to(torch.int16)
-
-
-def load_oracle_weight_codes(model, cfg) -> int:
-    """Binds the oracle's weight codes to every quantized layer of `model` (identical int4 weights).
-    Returns the number of layers."""
-    from quantized_vit_amd.quant_layers import QuantizeMixin
-    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
-    n = 0
-    for name, m in model.named_modules():
-        if isinstance(m, QuantizeMixin):
-            m.load_weight_codes(oracle_weight_codes(sd, name, cfg.quant_type, cfg.quant_mode))
-            n += 1
-    return n
-
-
-def gpu_codes_by_prefix(model, trace: dict, img_shape) -> Dict[str, torch.Tensor]:
-    """quant_layers.CODE_TRACE (layer -> codes) keyed by module name, in the oracle's layout."""
-    names = {m: n for n, m in model.named_modules()}
-    out = {}
-    for layer, codes in trace.items():
-        name = names[layer]
-        c = codes.cpu()
-        if name == "patch_embed.proj":
-            B, Cin, H, W = img_shape
-            p = layer.kernel_size[0]
-            gh, gw = H // p, W // p
-            # im2col rows (b, patch) x (c, kh, kw)  ->  NCHW image codes (patches do not overlap)
-            c = c.reshape(B, gh, gw, Cin, p, p).permute(0, 3, 1, 4, 2, 5).reshape(B, Cin, H, W)
-        out[name] = c
-    return out
-
-
-class TieResolvingHook:
-    """oracle act_hook adopting the GPU's code at proven ties (see the module docstring)."""
-
-    def __init__(self, gpu_codes: Dict[str, torch.Tensor]):
-        self.gpu = gpu_codes
-        self.stats: Dict[str, dict] = {}
-
-    def __call__(self, prefix: str, x: torch.Tensor, q: "O.LayerQ") -> torch.Tensor:
-        if q.quant_mode != O.WEIGHT_AND_ACTIVATION:
-            return x
-        own = O.quant_codes(x, q.quant_type, q.d_act, q.q_m_act, q.t_act)
-        g = self.gpu.get(prefix)
-        if g is None:
-            self.stats[prefix] = {"missing": True}
-            use = own
-        else:
-            g = g.to(own.dtype)
-            if prefix != "patch_embed.proj":
-                g = g.reshape(own.shape)
-            st = tie_check(x, g, own, q.quant_type, q.d_act, q.q_m_act, q.t_act)
-            self.stats[prefix] = st
-            # adopt the GPU's codes only when every difference is a proven tie (a failure is reported
-            # by the stats; the oracle then keeps its own codes)
-            use = g if st["non_ties"] == 0 else own
-        return O._t(q.d_act) * use
-
-
-def tie_resolved_vit_check(model, cfg, img, dev, flip_budget: float = 1e-4) -> dict:
-    """Runs the GPU forward with its quantizer boundaries traced, then the oracle with proven ties
-    adopted. Returns {"rel": logits rel. error, "stats": per-layer tie statistics}."""
-    from quantized_vit_amd import quant_layers
-    quant_layers.CODE_TRACE = {}
-    try:
-        with torch.no_grad():
-            y = model(img.to(dev)).cpu()
-        trace = quant_layers.CODE_TRACE
-    finally:
-        quant_layers.CODE_TRACE = None
-    gpu = gpu_codes_by_prefix(model, trace, tuple(img.shape))
-    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
-    hook = TieResolvingHook(gpu)
-    with torch.no_grad():
-        ref = O.vit_forward(sd, cfg, img, act_hook=hook)
-    rel = ((y.double() - ref.double()).norm() / ref.double().norm()).item()
-    missing = [p for p, s in hook.stats.items() if s.get("missing")]
-    bad = {p: s for p, s in hook.stats.items() if not s.get("missing") and
-           (s["non_ties"] > 0 or s["flips"] > max(1, flip_budget * s["total"]))}
-    return {"rel": rel, "stats": hook.stats, "missing": missing, "bad": bad,
-            "flips": sum(s.get("flips", 0) for s in hook.stats.values()),
-            "codes": sum(s.get("total", 0) for s in hook.stats.values())}
+"""The tie-resolved parity checker lives with the oracle (oracle/ties.py); re-exported for the tests."""
+from oracle.ties import (TIE_TOL, TieResolvingHook, code_position, gpu_codes_by_prefix,  # noqa: F401
+                         load_oracle_weight_codes, oracle_weight_codes, tie_check, tie_resolved_vit_check)

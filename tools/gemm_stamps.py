@@ -27,10 +27,6 @@ def main():
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--shapes", default="fc1_i32,fc1,qkv,fc2")
     ap.add_argument("--iters", type=int, default=5)
-    ap.add_argument("--abl", type=int, nargs="*", default=[1, 4, 5],
-                    help="with --build: also build timing-only ablation libraries (1 no DMA, "
-                         "4 contiguous L2-hot pieces, 5 per-row pieces on L2-hot rows)")
-    ap.add_argument("--bench-abl", type=int, default=0, help="time ablation library N (no stamps)")
     ap.add_argument("--build-var", nargs="*", default=[],
                     help="NAME=DEF1,DEF2 ...: build tools/_diag/libqvit_hip_NAME.so with those defines")
     ap.add_argument("--bench-var", default="", help="time variant library NAME (see --build-var)")
@@ -43,20 +39,15 @@ def main():
                               lib=os.path.join(DIAG, f"libqvit_hip_{name}.so"),
                               build_dir=os.path.join(DIAG, f"obj_{name}")))
         return
-    if a.bench_var:
-        a.bench_abl = a.bench_var
     if a.build:
         print(build.build(defines=("QVIT_GEMM_STAMPS",), lib=LIB, build_dir=os.path.join(DIAG, "obj")))
-        for n in a.abl:
-            print(build.build(defines=(f"QVIT_GEMM_ABL={n}",), lib=os.path.join(DIAG, f"libqvit_hip_abl{n}.so"),
-                              build_dir=os.path.join(DIAG, f"obj_abl{n}")))
         return
-    if a.bench_abl:
+    if a.bench_var:
         import torch
         from quantized_vit_amd import _lib
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         import gemm_bench
-        tag = a.bench_abl if isinstance(a.bench_abl, str) else f"abl{a.bench_abl}"
+        tag = a.bench_var
         _lib.load(os.path.join(DIAG, f"libqvit_hip_{tag}.so"))
         for name in a.shapes.split(","):
             M, N, K, epi = gemm_bench.SHAPES[name]
