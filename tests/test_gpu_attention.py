@@ -285,9 +285,12 @@ def _split_path(dev, B, N, H, A, packed, npad, kpad, bias_pad, da, dw, s, out, m
     return out.cpu()
 
 
-@pytest.mark.parametrize("B,N,H", [(3, 197, 12), (2, 50, 4), (1, 208, 2), (5, 1, 3), (2, 17, 12), (9, 100, 1)])
-def test_qkv_attention_fused_f32_vs_split_path(dev, B, N, H):
-    A, packed, npad, kpad, bias_pad, da, dw = _fused_case(dev, B, N, H, seed=B * 1000 + N + H)
+# K != 768 runs the runtime-K projection loop (NKC = 0), K = 768 the unrolled one
+@pytest.mark.parametrize("B,N,H,K", [(3, 197, 12, 768), (2, 50, 4, 768), (1, 208, 2, 768), (5, 1, 3, 768),
+                                     (2, 17, 12, 768), (9, 100, 1, 768), (3, 197, 8, 512), (2, 197, 12, 1024),
+                                     (40, 197, 3, 256)])
+def test_qkv_attention_fused_f32_vs_split_path(dev, B, N, H, K):
+    A, packed, npad, kpad, bias_pad, da, dw = _fused_case(dev, B, N, H, seed=B * 1000 + N + H, K=K)
     ref = _split_path(dev, B, N, H, A, packed, npad, kpad, bias_pad, da, dw, 2.0 ** -2,
                       torch.full((B * N, 64 * H), float("nan"), device=dev), _lib.ATT_F32)
     out = torch.full((B * N, 64 * H), float("nan"), device=dev)
