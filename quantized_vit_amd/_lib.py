@@ -271,10 +271,10 @@ def qkv_attention(codes: torch.Tensor, B: int, N: int, K: int, packed: torch.Ten
                   d_act: torch.Tensor, d_wt: torch.Tensor, bias_pad: Optional[torch.Tensor], H: int, scale: float,
                   out: torch.Tensor, out_mode: int = ATT_F32, in_scale: float = 1.0, out_qtype: int = 0,
                   out_d=None, out_qm=None, out_t=None, out_levels: int = 0,
-                  epi_table: Optional[torch.Tensor] = None) -> torch.Tensor:
+                  epi_table: Optional[torch.Tensor] = None, wfmt: int = W4) -> torch.Tensor:
     """qkv projection (W4 codes) + attention core in one kernel (qvit_qkv_attention), N <= 208."""
     _require_gpu(codes, "codes")
-    _check(load().qvit_qkv_attention(_ptr(codes), B, N, K, codes.stride(0), _ptr(packed), W4, npad, _ptr(d_act),
+    _check(load().qvit_qkv_attention(_ptr(codes), B, N, K, codes.stride(0), _ptr(packed), wfmt, npad, _ptr(d_act),
                                      _ptr(d_wt), _ptr(bias_pad), H, 64, scale, in_scale, out_mode, _ptr(out),
                                      out.stride(0), out_qtype, _ptr(out_d), _ptr(out_qm), _ptr(out_t), out_levels,
                                      _ptr(epi_table), _stream(codes.device)), "qvit_qkv_attention")

@@ -165,24 +165,6 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const float* __restrict__ 
 // previous block is computed, with no register staging and no conversion in this kernel.
 constexpr int SRING = 4;
 
-QVIT_DEV uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-
-// 64 lanes x 16 B from per-lane global addresses to lds_base + 16 * lane (M0 saved and restored).
-QVIT_DEV void dma16(const void* gsrc, uint32_t lds_base) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gsrc), "s"(lds_base)
-      : "memory");
-}
-
 template <int N_>
 QVIT_DEV void block_sync() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N_) : "memory");

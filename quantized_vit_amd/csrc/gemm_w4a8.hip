@@ -81,40 +81,6 @@ QVIT_DEV int lane_opaque() {
   return l;
 }
 
-QVIT_DEV uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-
-// One 1-KiB LDS-DMA piece: 64 lanes x 16 B from per-lane global addresses to lds_base + 16*lane.
-// Issued from asm so the compiler neither counts it nor drains vmcnt for it; M0 is saved/restored.
-QVIT_DEV void dma16(const void* gsrc, uint32_t lds_base) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gsrc), "s"(lds_base)
-      : "memory");
-}
-
-// The same from a wave-uniform SGPR base + a per-lane 32-bit byte offset (the global "saddr" form): no
-// 64-bit per-lane address arithmetic and no VGPR pair holding a base pointer across the main loop.
-QVIT_DEV void dma16s(const void* sbase, uint32_t voff, uint32_t lds_base) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %3\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, %2\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(sbase), "s"(lds_base)
-      : "memory");
-}
-
 // Wait until at most N of this wave's DMAs are in flight, retire its LDS reads, then barrier.
 // The LDS drain is the builtin (lgkmcnt(0) = 0xC07F on gfx9) so the compiler's wait-count model sees
 // it and does not re-drain lgkmcnt when the next stage's fragment reads are in flight.

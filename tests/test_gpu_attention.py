@@ -336,6 +336,7 @@ def test_qkv_attention_argument_validation(dev):
     assert lib.qvit_qkv_attention(*args()) == 0
     assert lib.qvit_qkv_attention(*args(N=209)) == -1        # N > 208
     assert lib.qvit_qkv_attention(*args(wfmt=8)) == -1       # int4 weights only
+    assert lib.qvit_qkv_attention(*args(B=1 << 17, N=200, lda=1 << 8)) == -1   # A past 32-bit offsets
     assert lib.qvit_qkv_attention(*args(K=128, lda=256)) == -1   # K % 256
     assert lib.qvit_qkv_attention(*args(hd=32)) == -1
     assert lib.qvit_qkv_attention(*args(A=None)) == -3

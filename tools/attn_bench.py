@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--split-only", action="store_true")
     ap.add_argument("--fused", action="store_true", help="also time qvit_qkv_attention (+ the qkv split GEMM)")
     ap.add_argument("--stamps", action="store_true", help="with a -DQVIT_ATT_STAMPS --lib: phase cycles")
+    ap.add_argument("--w8", action="store_true", help="fused kernel on the int8 image (a diagnostic --lib)")
     a = ap.parse_args()
     if a.lib:
         _lib.load(a.lib)
@@ -86,13 +87,19 @@ def main():
         acodes = torch.randint(-60, 61, (B * N, 768), generator=g)
         w = torch.randint(-7, 8, (3 * C, 768), generator=g)
         packed, npad, kpad = pack_codes(w, _lib.W4, dev)
+        packed8, _, _ = pack_codes(w, _lib.W8, dev)
         bias_pad = _lib.pad_bias((torch.randn(3 * C, generator=g) * 0.3).to(dev), 3 * C, npad, dev)
         A = act_buffer(acodes, kpad, dev)
         da, dw = torch.tensor([0.004], device=dev), torch.tensor([0.003], device=dev)
-        fz = lambda: _lib.qkv_attention(A, B, N, kpad, packed, npad, da, dw, bias_pad, H, 0.125, codes, _lib.ATT_I8,
-                                        1.0, _lib.QT_NONLINEAR, d, qm, t, epi_table=table)
+        wimg, wf = (packed8, _lib.W8) if a.w8 else (packed, _lib.W4)
+        fz = lambda: _lib.qkv_attention(A, B, N, kpad, wimg, npad, da, dw, bias_pad, H, 0.125, codes, _lib.ATT_I8,
+                                        1.0, _lib.QT_NONLINEAR, d, qm, t, epi_table=table, wfmt=wf)
         ms = timeit(fz, a.iters)
         print(f"{'fused qkv+attn i8':20s} {ms*1e3:9.1f} us", flush=True)
+        outf = torch.empty(B * N, C, device=dev)
+        ms = timeit(lambda: _lib.qkv_attention(A, B, N, kpad, wimg, npad, da, dw, bias_pad, H, 0.125, outf,
+                                               _lib.ATT_F32, 1.0, wfmt=wf), a.iters)
+        print(f"{'fused qkv+attn f32':20s} {ms*1e3:9.1f} us", flush=True)
         hi2 = torch.empty(B * N * 3 * C, dtype=torch.float16, device=dev)
         lo2 = torch.empty_like(hi2)
         ms2 = timeit(lambda: _lib.gemm_qkv_split(A, B * N, kpad, packed, _lib.W4, 3 * C, npad, da, dw, bias_pad, N, 1.0,
