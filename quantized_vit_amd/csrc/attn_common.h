@@ -49,11 +49,13 @@ QVIT_DEV f4 mfma3(h8 ah, h8 al, h8 bh, h8 bl, f4 c) {
 
 // Cross-lane max / sum over the 4 lane groups g (xor 16, xor 32) with the gfx950 permlane swaps (VALU,
 // no LDS round trip); the sums add in the same order as a butterfly of shuffles.
+// (scores are never NaN: IEEE maximum, v_maximum3_f32 on gfx950, needs none of fmaxf's operand quieting)
+QVIT_DEV float fmax_nn(float a, float b) { return __builtin_elementwise_maximum(a, b); }
 QVIT_DEV float xmax(float v) {
   const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  v = fmax_nn(__uint_as_float(a[0]), __uint_as_float(a[1]));
   const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+  return fmax_nn(__uint_as_float(b[0]), __uint_as_float(b[1]));
 }
 QVIT_DEV float xsum(float v) {
   const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
@@ -159,7 +161,7 @@ QVIT_DEV void attend(int nt, bool mask, const int8_t* st, const h8 (&qh)[T][2], 
 #pragma unroll
       for (int e = 0; e < 8; ++e) r[e] = (kbase + 16 * (e >> 2) + (e & 3) < N) ? r[e] : -INFINITY;
     }
-    float bm = fmaxf(fmaxf(fmaxf(r[0], r[1]), fmaxf(r[2], r[3])), fmaxf(fmaxf(r[4], r[5]), fmaxf(r[6], r[7])));
+    float bm = fmax_nn(fmax_nn(fmax_nn(r[0], r[1]), fmax_nn(r[2], r[3])), fmax_nn(fmax_nn(r[4], r[5]), fmax_nn(r[6], r[7])));
     bm = xmax(bm) * sl2;
 #if QVIT_ATT_DEFER
     // deferred max: the running max moves only when some query's block max exceeds it by more than 8
@@ -168,7 +170,7 @@ QVIT_DEV void attend(int nt, bool mask, const int8_t* st, const h8 (&qh)[T][2], 
     if (__builtin_amdgcn_ballot_w64(bm > m[i] + 8.f) != 0)
 #endif
     {
-      const float mn = fmaxf(m[i], bm);
+      const float mn = fmax_nn(m[i], bm);
       const float alpha = __builtin_amdgcn_exp2f(m[i] - mn);
       l[i] *= alpha;
 #pragma unroll

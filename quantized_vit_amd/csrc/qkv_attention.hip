@@ -112,8 +112,8 @@ QVIT_DEV void attend_f(const int8_t* st, const h8 (&qh)[TPW][2], const h8 (&ql)[
       r[i][e] = s[i][e >> 2][e & 3];
       if (MASK) r[i][e] = (kbase + 16 * (e >> 2) + (e & 3) < N) ? r[i][e] : -INFINITY;
     }
-    const float b0 = fmaxf(fmaxf(fmaxf(r[i][0], r[i][1]), fmaxf(r[i][2], r[i][3])),
-                           fmaxf(fmaxf(r[i][4], r[i][5]), fmaxf(r[i][6], r[i][7])));
+    const float b0 = fmax_nn(fmax_nn(fmax_nn(r[i][0], r[i][1]), fmax_nn(r[i][2], r[i][3])),
+                             fmax_nn(fmax_nn(r[i][4], r[i][5]), fmax_nn(r[i][6], r[i][7])));
     bm[i] = xmax(b0) * sl2;
     grow |= bm[i] > m[i] + 8.f;
   }
@@ -122,7 +122,7 @@ QVIT_DEV void attend_f(const int8_t* st, const h8 (&qh)[TPW][2], const h8 (&ql)[
   if (__builtin_amdgcn_ballot_w64(grow) != 0) {
 #pragma unroll
     for (int i = 0; i < NTV; ++i) {
-      const float mn = fmaxf(m[i], bm[i]);
+      const float mn = fmax_nn(m[i], bm[i]);
       const float alpha = __builtin_amdgcn_exp2f(m[i] - mn);
       l[i] *= alpha;
 #pragma unroll
