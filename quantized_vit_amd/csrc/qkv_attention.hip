@@ -23,9 +23,6 @@
 #include <algorithm>
 #include <type_traits>
 
-#ifndef QVIT_QA_DIAG
-#define QVIT_QA_DIAG 0
-#endif
 
 namespace {
 
@@ -234,11 +231,7 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
   const uint32_t lane16 = 16u * (uint32_t)lane;
   // weight k-step s of a unit -> ring slot rs: this wave's DMA piece
   auto dma_piece = [&](const Src& sr, int s, int rs) __attribute__((always_inline)) {
-#if QVIT_QA_DIAG == 2
-    dma16s(Wp + sr.w, lane16, lds_w + (uint32_t)(rs * WSLOT));
-#else
     dma16s(Wp + sr.w + (uint32_t)s * (uint32_t)IMG4_STEP, lane16, lds_w + (uint32_t)(rs * WSLOT));
-#endif
   };
   // activation loads walk one running offset per tile (+64 B per k-step, reset to the next unit's rows when
   // the stream crosses into it), advanced by asm so the compiler cannot precompute (and hold) every
@@ -249,11 +242,7 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
   uint32_t aoff[TPW];
   auto act_load = [&](v4i& xd, int tt) __attribute__((always_inline)) {
     xd = *reinterpret_cast<const v4i*>(A + (size_t)aoff[tt]);
-#if QVIT_QA_DIAG != 1
     asm volatile("v_add_u32_e32 %0, 64, %0" : "+v"(aoff[tt]));
-#else
-    asm volatile("v_add_u32_e32 %0, 0, %0" : "+v"(aoff[tt]));
-#endif
   };
   auto act_next = [&](v4i (&xd)[TPW]) __attribute__((always_inline)) {
 #pragma unroll
@@ -335,12 +324,8 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
       v4i wc = unpack16(wfr[0]);
 #pragma unroll
       for (int f = 0; f < 12; ++f) {
-#if QVIT_QA_DIAG == 4
-        asm volatile("" :: "v"(wc), "v"(xa[q][0]), "v"(xa[q][1]));
-#else
         acc[0][f] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wc, xa[q][0], acc[0][f], 0, 0, 0);
         if (decltype(two)::value) acc[1][f] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wc, xa[q][1], acc[1][f], 0, 0, 0);
-#endif
         if (f < 11) wc = unpack16(wfr[f + 1]);
         if (more) wfr[f] = wfrag(rn, f);
         if (f == 0) {  // weight k-step s + 3 (past the unit's end: the next unit's 0, 1, 2)
@@ -455,10 +440,8 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
       if (nfull < nkb)
         attend_f<NTV, true>(kv + nfull * KB * 128, qh, ql, m, l, o, koffs, voffs, nfull * KB + 4 * fq, N, sl2);
     };
-    if (QVIT_QA_DIAG != 3) {
-      if (nt == 2) attend_all(std::integral_constant<int, 2>{});
-      else if (nt == 1) attend_all(std::integral_constant<int, 1>{});
-    }
+    if (nt == 2) attend_all(std::integral_constant<int, 2>{});
+    else if (nt == 1) attend_all(std::integral_constant<int, 1>{});
     sp.mark(0);
     attend_store<OUT, TPW>(tv, l, o, wr, FW, 0, N, b, h, in_scale, out, ldo, qp, tb, st16);
     sp.mark(4);
