@@ -2,20 +2,20 @@
 //   qkv = QuantizeLinear(x_codes)  ->  softmax(q k^T * scale) v  ->  proj's activation quantizer
 // with q, k, v never leaving the chip. One persistent workgroup (8 waves) per CU walks (image, head)
 // units; per unit:
-//   1. projection: wave w computes the 192 q|k|v features of its token tiles {w', w'+8} (w' = w rotated
-//      by unit) on v_mfma_i32_16x16x64_i8, as a GEMM-style pipeline: the head's three 64-row weight groups
+//   1. projection: wave w computes the 192 q|k|v features of its token tiles {2 w', 2 w' + 1} (w' = w
+//      rotated by unit) on v_mfma_i32_16x16x64_i8, as a GEMM-style pipeline: the head's three 64-row weight groups
 //      of each 64-deep k-step are LDS-DMA'd (global_load_lds, 6 x 1 KiB, no register staging) from the
 //      GEMM's pre-tiled int4 image into a 4-slot ring three k-steps ahead; activation fragments go global
 //      -> registers three k-steps ahead; one counted vmcnt + barrier per k-step; the MFMAs of k-step s run
 //      while the packed weight fragments of k-step s+1 are read from LDS, each unpacked to 16x-scaled int8
 //      right before its two MFMAs;
 //   2. epilogue: v = (d_a d_w acc + bias) * in_scale split into fp16 hi/lo exactly as
-//      qvit_gemm_qkv_split does; q stays in registers as the wave's own S^T B-operand fragments (the
-//      contraction runs over the head dims in the order the accumulators hold them: lane group g owns
-//      dims 16g .. 16g+15), k and v go to resident LDS images (208 rows, XOR-swizzled);
-//   3. attention: the 7 key blocks of 32 with no barrier (K/V resident), online softmax, P·V, and the
-//      output quantizer through its code table (attn_common.h, same arithmetic as qvit_attention_split
-//      except the order of the dims inside each q·k sum).
+//      qvit_gemm_qkv_split does; q stays in registers (one permlane16 swap turns the two tiles into the
+//      32-query tile's S^T B operands), k and v go to resident LDS images (208 rows, XOR-swizzled);
+//   3. attention on v_mfma_f32_32x32x16_f16 (one 32-query tile per wave): the 7 key blocks of 32 with no
+//      barrier (K/V resident), block kb + 1's scores issued ahead of block kb's online softmax, P·V, and
+//      the output quantizer through its code table (same arithmetic as qvit_attention_split except the
+//      order of the terms inside the q·k, P·V and row sums, and a running max kept an integer).
 // The next unit's first weight k-steps (ring) and activation k-steps (registers) load while the current
 // unit's attention runs. N <= 208.
 #include "attn_common.h"
@@ -60,91 +60,219 @@ QVIT_DEV v4i unpack16(uint2 p) {
   return v4i{(int)nib16_lo(p.x), (int)nib16_hi(p.x), (int)nib16_lo(p.y), (int)nib16_hi(p.y)};
 }
 
-// Online-softmax update of one key block for the fused kernel's NTV (1 or 2) query tiles: attn_common.h's
-// attend with the branches taken out of the block body. The tile count and the mask (last block only)
-// are template parameters, and one ballot per block decides the deferred rescale for all tiles (a tile
-// whose own max did not move past its bound is rescaled along, to max(m, block max): still within 2^8
-// of every score), so the P computation and the P.V products of both tiles form one branch-free region
-// the scheduler can interleave.
-template <int NTV, bool MASK>
-QVIT_DEV void attend_f(const int8_t* st, const h8 (&qh)[TPW][2], const h8 (&ql)[TPW][2], float (&m)[TPW],
-                       float (&l)[TPW], f4 (&o)[TPW][4], const int (&koffs)[2][2], const int (&voffs)[4], int kbase,
-                       int N, float sl2) {
-  f4 s[NTV][2];
-  // the last block's second 16 keys all past N (N % 32 in 1..16): their scores are masked, skip them
-  const bool half = MASK && (kbase & ~31) + 16 >= N;  // kbase = block start + 4 g, g < 4
-  {
-    h8 kh[2][2], kl[2][2];
+// ---- attention on v_mfma_f32_32x32x16_f16 --------------------------------------------------------------
+// A wave's two 16-query tiles are one 32-query tile (query r < 16: tile 0, else tile 1, token r & 15). Per key
+// block of 32: S^T = K . Q^T (keys x queries, 4 dim chunks x 3 passes), then O^T += V^T . P^T (2 32-dim tiles x
+// 2 key chunks x 3 passes): 24 MFMAs that hold the SIMD's vector issue 8 of 32 cycles each, instead of 48
+// 16x16x32 ones that hold it 8 of 16 (the phase is issue-bound). A lane (r = lane & 31, h = lane >> 5) owns
+// query r: S^T's accumulator holds its scores of keys (e & 3) + 8 (e >> 2) + 4 h (e < 16), the other 16 are
+// in lane ^ 32, so a row max / sum is 15 in-lane steps and one permlane32 swap.
+// The contraction orders: the q . k sum of MFMA chunk c runs over dims 32 h + 8 c + j (K's 16-B chunk 4 h + c,
+// the layout koff already has); the P . V sum over chunk kc takes S^T's registers 8 kc .. 8 kc + 7 as its
+// B operand with no lane movement, so element j of half h is key 16 kc + 8 (j >> 2) + 4 h + (j & 3), and V^T
+// is read (ds_read_b64_tr_b16) in that same key order.
+typedef float f16x __attribute__((ext_vector_type(16)));
+
+QVIT_DEV f16x mfma3w(h8 ah, h8 al, h8 bh, h8 bl, f16x c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, c, 0, 0, 0);
+  return c;
+}
+
+// V image of the fused kernel: 128-B rows, 16-B chunks XOR-swizzled by row bits 1 and 2 only, so the transposed
+// reads of 4 consecutive rows x 64 B (one 32-lane pass) cover all 64 banks, and a read 8, 16 or 32 rows further
+// keeps the same swizzle (an immediate offset); the epilogue's 16-B writes are 2-way
+QVIT_DEV int v32off(int r, int byte) { return r * 128 + (byte ^ (((((r >> 1) & 1) << 2) | ((r >> 2) & 1)) << 4)); }
+
+// P's fp16 hi/lo split with the same values as attn_common.h split8 (hi = RNE f16 of x; lo = RNE f16 of the
+// exact f32 x - hi) in fewer VALU: lo comes from v_fma_mix{lo,hi}_f16 (-hi as an f16 source, x as f32, one
+// rounding of the exact difference) instead of cvt f16 -> f32, subtract and cvt back. The asm carries its own
+// wait states: s_nop 0 first (x is fresh from v_exp: transcendental -> VALU use), s_nop 1 last (its results
+// are MFMA operands: VALU write -> MFMA read).
+QVIT_DEV void split8_mix(const float (&x)[8], h8& hi, h8& lo) {
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
+  for (int i = 0; i < 8; ++i) hi[i] = (_Float16)x[i];
+  const u4 hw = __builtin_bit_cast(u4, hi);
+  u4 lw;
+  asm("s_nop 0\n\t"
+      "v_fma_mixlo_f16 %0, -%4, 1.0, %8 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, -%4, 1.0, %9 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixlo_f16 %1, -%5, 1.0, %10 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %1, -%5, 1.0, %11 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixlo_f16 %2, -%6, 1.0, %12 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %2, -%6, 1.0, %13 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixlo_f16 %3, -%7, 1.0, %14 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %3, -%7, 1.0, %15 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "s_nop 1"
+      : "=&v"(lw[0]), "=&v"(lw[1]), "=&v"(lw[2]), "=&v"(lw[3])
+      : "v"(hw[0]), "v"(hw[1]), "v"(hw[2]), "v"(hw[3]), "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]),
+        "v"(x[5]), "v"(x[6]), "v"(x[7]));
+  lo = __builtin_bit_cast(h8, lw);
+}
+
+QVIT_DEV float bits_f(uint32_t u) { return __uint_as_float(u); }
+QVIT_DEV float pair_max(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmax_nn(bits_f(a[0]), bits_f(a[1]));
+}
+QVIT_DEV float pair_sum(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return bits_f(a[0]) + bits_f(a[1]);
+}
+
+// S^T of one key block (st: the block's first K hi row)
+QVIT_DEV f16x scores32(const int8_t* st, const h8 (&qh)[4], const h8 (&ql)[4], const int (&koffs)[4]) {
+  h8 kh[4], kl[4];
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        if (kt == 1 && half) continue;
-        kh[kt][c] = lds_h8(st, koffs[kt][c]);
-        kl[kt][c] = lds_h8(st + IMGF, koffs[kt][c]);
-      }
-#pragma unroll
-    for (int i = 0; i < NTV; ++i)
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        s[i][kt] = f4{0.f, 0.f, 0.f, 0.f};
-        if (kt == 1 && half) continue;  // wave-uniform
-#pragma unroll
-        for (int c = 0; c < 2; ++c) s[i][kt] = mfma3(kh[kt][c], kl[kt][c], qh[i][c], ql[i][c], s[i][kt]);
-      }
+  for (int c = 0; c < 4; ++c) {
+    kh[c] = lds_h8(st, koffs[c]);
+    kl[c] = lds_h8(st + IMGF, koffs[c]);
   }
+  f16x s = {};
+#pragma unroll
+  for (int c = 0; c < 4; ++c) s = mfma3w(kh[c], kl[c], qh[c], ql[c], s);
+  return s;
+}
+
+// Online-softmax update of one key block from its scores s. Deferred running max as in attn_common.h
+// attend: m moves only when the block max exceeds it by more than 8 (log2 units), so P <= 2^8 is exact in
+// the fp16 hi/lo split. MASK: the block holds keys >= N (the last block only).
+template <bool MASK>
+QVIT_DEV void softmax_pv32(const int8_t* st, const f16x& s, float& m, float& l, f16x (&o)[2],
+                           const int (&voffs)[2], int kbase, int N, float sl2) {
   // V fragments of the block issued before the softmax (they land while it runs)
-  h8 vh[4], vl[4];
+  h8 vh[2][2], vl[2][2];
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt) {
-    vh[dt] = join(tr_read(st + 2 * IMGF, voffs[dt]), tr_read(st + 2 * IMGF, voffs[dt] + 16 * 128));
-    vl[dt] = join(tr_read(st + 3 * IMGF, voffs[dt]), tr_read(st + 3 * IMGF, voffs[dt] + 16 * 128));
-  }
-  float r[NTV][8], bm[NTV];
-  bool grow = false;
+  for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
-  for (int i = 0; i < NTV; ++i) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      r[i][e] = s[i][e >> 2][e & 3];
-      if (MASK) r[i][e] = (kbase + 16 * (e >> 2) + (e & 3) < N) ? r[i][e] : -INFINITY;
+    for (int kc = 0; kc < 2; ++kc) {
+      const int o0 = voffs[dt] + 16 * kc * 128;  // voffs includes the V hi image's 2 IMGF
+      vh[dt][kc] = join(tr_read(st, o0), tr_read(st, o0 + 8 * 128));
+      vl[dt][kc] = join(tr_read(st + IMGF, o0), tr_read(st + IMGF, o0 + 8 * 128));
     }
-    const float b0 = fmax_nn(fmax_nn(fmax_nn(r[i][0], r[i][1]), fmax_nn(r[i][2], r[i][3])),
-                             fmax_nn(fmax_nn(r[i][4], r[i][5]), fmax_nn(r[i][6], r[i][7])));
-    bm[i] = xmax(b0) * sl2;
-    grow |= bm[i] > m[i] + 8.f;
+  float r[16];
+  const int h4 = 4 * ((threadIdx.x >> 5) & 1);
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    r[e] = s[e];
+    if (MASK) r[e] = (kbase + (e & 3) + 8 * (e >> 2) + h4 < N) ? r[e] : -INFINITY;
   }
-  // deferred running max (attn_common.h attend): moved only when some query's block max exceeds it by
-  // more than 8 in log2 units, so P <= 2^8 (exact in the fp16 hi/lo split)
-  if (__builtin_amdgcn_ballot_w64(grow) != 0) {
+  // 16 scores -> one max in 8 v_maximum3_f32
+  float t[5];
 #pragma unroll
-    for (int i = 0; i < NTV; ++i) {
-      const float mn = fmax_nn(m[i], bm[i]);
-      const float alpha = __builtin_amdgcn_exp2f(m[i] - mn);
-      l[i] *= alpha;
+  for (int e = 0; e < 5; ++e) t[e] = fmax_nn(fmax_nn(r[3 * e], r[3 * e + 1]), r[3 * e + 2]);
+  const float b0 = fmax_nn(fmax_nn(fmax_nn(t[0], t[1]), t[2]), fmax_nn(fmax_nn(t[3], t[4]), r[15]));
+  const float bm = pair_max(b0) * sl2;
+  // deferred rescale (rare after the first block). The running max is kept an integer (ceil), so alpha is a
+  // power of two and the rescale is an exact v_ldexp_f32 per accumulator: scalar, where a compiler multiply is
+  // SLP-packed into v_pk_mul_f32 (packed f32 VALU beside the MFMAs costs several times its issue slot)
+  if (__builtin_amdgcn_ballot_w64(bm > m + 8.f) != 0) {
+    const float mn = __builtin_ceilf(fmax_nn(m, bm));
+    const int k = (int)fmax_nn(m - mn, -256.f);  // m starts at -2^30: the first block scales 0 by 2^-256
+    l = __builtin_amdgcn_ldexpf(l, k);
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) o[i][dt] = o[i][dt] * alpha;
-      m[i] = mn;
+    for (int e = 0; e < 16; ++e) {
+      o[0][e] = __builtin_amdgcn_ldexpf(o[0][e], k);
+      o[1][e] = __builtin_amdgcn_ldexpf(o[1][e], k);
+    }
+    m = mn;
+  }
+  const float nm = -m;
+  float x[2][8];
+  float ps = 0.f;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    x[e >> 3][e & 7] = __builtin_amdgcn_exp2f(fmaf(r[e], sl2, nm));
+    ps += x[e >> 3][e & 7];
+  }
+  l += ps;
+  h8 ph[2], pl[2];
+  split8_mix(x[0], ph[0], pl[0]);
+  split8_mix(x[1], ph[1], pl[1]);
+#pragma unroll
+  for (int kc = 0; kc < 2; ++kc)
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) o[dt] = mfma3w(vh[dt][kc], vl[dt][kc], ph[kc], pl[kc], o[dt]);
+}
+
+// Normalise and write the wave's 32 queries: fp32 rows, or the next layer's int8 codes. o[dt][4 g + j] is dim
+// 32 dt + 8 g + 4 h + j of the lane's query; with st16 the two halves trade words (permlane32) so that each
+// lane stores 16 contiguous codes per 32-dim tile (half h: dims 32 dt + 16 h .. + 15).
+template <int OUT>
+QVIT_DEV void attend_store32(const bool (&tv)[TPW], float l, const f16x (&o)[2], int wr, int N, int b, int h,
+                             float in_scale, void* out, int64_t ldo, const QParams& qp, const EpiLds& tb, bool st16) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 31, hh = lane >> 5;
+  const int tile = r >> 4;
+  const float inv = 1.f / (pair_sum(l) * in_scale);
+  const int q = 16 * (2 * wr + tile) + (r & 15);
+  const bool ok = (tile ? tv[1] : tv[0]) && q < N;
+  const int64_t row = (int64_t)b * N + q;
+  if (OUT == 0) {
+    if (!ok) return;
+    float* dst = reinterpret_cast<float*>(out) + row * ldo + h * HD + 4 * hh;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<f4*>(dst + 32 * dt + 8 * g) =
+            f4{o[dt][4 * g], o[dt][4 * g + 1], o[dt][4 * g + 2], o[dt][4 * g + 3]} * inv;
+    return;
+  }
+  uint32_t wd[2][4];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    if (tb.ent != nullptr) {
+      float v[4][4];
+      uint2 e[4][4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[g][j] = o[dt][4 * g + j] * inv;
+          e[g][j] = *epi_entry(tb.ent, v[g][j], tb.c0, tb.inv_w, tb.top);
+        }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        epi_select_byte<0>(wd[dt][g], v[g][0], __uint_as_float(e[g][0].x), e[g][0].y);
+        epi_select_byte<1>(wd[dt][g], v[g][1], __uint_as_float(e[g][1].x), e[g][1].y);
+        epi_select_byte<2>(wd[dt][g], v[g][2], __uint_as_float(e[g][2].x), e[g][2].y);
+        epi_select_byte<3>(wd[dt][g], v[g][3], __uint_as_float(e[g][3].x), e[g][3].y);
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float k[4];
+        bool need[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) k[j] = quant_fast(o[dt][4 * g + j] * inv, qp, need[j]);
+        if (need[0] | need[1] | need[2] | need[3]) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (need[j]) k[j] = quant_fixup(o[dt][4 * g + j] * inv, qp);
+        }
+        uint32_t word = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) word |= ((uint32_t)(uint8_t)to_i8_sat(k[j])) << (8 * j);
+        wd[dt][g] = word;
+      }
     }
   }
-  h8 ph[NTV], pl[NTV];
+  int8_t* dst = reinterpret_cast<int8_t*>(out) + row * ldo + h * HD;
+  if (st16) {
 #pragma unroll
-  for (int i = 0; i < NTV; ++i) {
-    const float nm = -m[i];
-    float x[8];
-    float ps = 0.f;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      x[e] = __builtin_amdgcn_exp2f(fmaf(r[i][e], sl2, nm));
-      ps += x[e];
+    for (int dt = 0; dt < 2; ++dt) {
+      const auto a = __builtin_amdgcn_permlane32_swap(wd[dt][0], wd[dt][2], false, false);
+      const auto c = __builtin_amdgcn_permlane32_swap(wd[dt][1], wd[dt][3], false, false);
+      if (ok) *reinterpret_cast<uint4*>(dst + 32 * dt + 16 * hh) = make_uint4(a[0], a[1], c[0], c[1]);
     }
-    l[i] += ps;
-    split8(x, ph[i], pl[i]);
+  } else if (ok) {
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) *reinterpret_cast<uint32_t*>(dst + 32 * dt + 8 * g + 4 * hh) = wd[dt][g];
   }
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int i = 0; i < NTV; ++i) o[i][dt] = mfma3(vh[dt], vl[dt], ph[i], pl[i], o[i][dt]);
 }
 
 // NKC: the number of 64-deep k-steps when fixed at compile time (12: K = 768, the ViT-B qkv; ViT-L's
@@ -220,7 +348,7 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
     const int wr = (wave + unit) & (FW - 1);
 #pragma unroll
     for (int tt = 0; tt < TPW; ++tt) {
-      int64_t m = (int64_t)b * N + 16 * (wr + FW * tt) + fr;
+      int64_t m = (int64_t)b * N + 16 * (2 * wr + tt) + fr;
       m = m < M ? m : M - 1;  // tokens past the image: rows of the next one (masked); clamp at the end
       sr.a[tt] = (uint32_t)(m * lda) + (uint32_t)(16 * fq);
     }
@@ -255,15 +383,17 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
     return *reinterpret_cast<const uint2*>(wbase + rs * WSLOT + (f >> 2) * WGRP + (f & 3) * 512);
   };
 
-  int koffs[2][2], voffs[4];
+  // attention fragment offsets (attend32): K row reads of key lane & 31, chunk 4 h + c; V^T transposed reads,
+  // lane 4 k + p of 16-lane group G supplies row 4 (G >> 1) + k, dims 32 dt + 16 (G & 1) + 4 p
+  int koffs[4], voffs[2];
 #pragma unroll
-  for (int kt = 0; kt < 2; ++kt)
+  for (int c = 0; c < 4; ++c) koffs[c] = koff(lane & 31, 4 * (lane >> 5) + c);
+  // (V's offsets carry the V hi image's start, hidden from the compiler: with 2 IMGF in the immediates the
+  // later blocks' offsets pass 64 KiB, and every block then needs base registers of its own)
 #pragma unroll
-    for (int c = 0; c < 2; ++c) koffs[kt][c] = koff(16 * kt + fr, 2 * fq + c);  // dims 16g + 8c .. +7
-  {
-    const int vq = fr >> 2, vp = fr & 3;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) voffs[dt] = voff(4 * fq + vq, 2 * (16 * dt + 4 * vp));
+  for (int dt = 0; dt < 2; ++dt) {
+    voffs[dt] = 2 * IMGF + v32off(4 * (fq >> 1) + (fr >> 2), 2 * (32 * dt + 16 * (fq & 1) + 4 * (fr & 3)));
+    asm volatile("" : "+v"(voffs[dt]));
   }
   const float sl2 = scale * LOG2E / (in_scale * in_scale);
   const bool st16 = ((ldo & 15) == 0) && ((((uintptr_t)out) & 15) == 0);
@@ -287,7 +417,7 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
     const int wr = (wave + unit) & (FW - 1);
     bool tv[TPW];
 #pragma unroll
-    for (int tt = 0; tt < TPW; ++tt) tv[tt] = wr + FW * tt < ntile;
+    for (int tt = 0; tt < TPW; ++tt) tv[tt] = 2 * wr + tt < ntile;
     const int nt = (tv[0] ? 1 : 0) + (tv[1] ? 1 : 0);
 
     // ---- 1. projection ---------------------------------------------------------------------------
@@ -311,8 +441,8 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
     //   (past the unit's end: the next unit's k-steps 0, 1, 2);
     //   MFMAs of k-step s: fragment f + 1 is unpacked while f's two MFMAs run, and each packed fragment is
     //   replaced by k-step s + 1's right after its MFMAs.
-    // TWO: the wave's second token tile is inside the image (otherwise its MFMAs are skipped: 3 of the 16
-    // tiles of N = 197). The order inside a k-step is pinned (sched_barrier); the DMA piece and the two
+    // two: 2 when both of the wave's token tiles {2 wr, 2 wr + 1} are inside the image, else 1 (the second
+    // tile's MFMAs are skipped; N = 197 has 13 tiles). The order inside a k-step is pinned (sched_barrier); the DMA piece and the two
     // activation loads go between the first fragments' MFMAs in that order (the next top's count).
     auto kstep = [&](auto two, int s, int q) __attribute__((always_inline)) {
       __builtin_amdgcn_sched_barrier(0);
@@ -324,8 +454,8 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
       v4i wc = unpack16(wfr[0]);
 #pragma unroll
       for (int f = 0; f < 12; ++f) {
-        acc[0][f] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wc, xa[q][0], acc[0][f], 0, 0, 0);
-        if (decltype(two)::value) acc[1][f] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wc, xa[q][1], acc[1][f], 0, 0, 0);
+        if (decltype(two)::value >= 1) acc[0][f] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wc, xa[q][0], acc[0][f], 0, 0, 0);
+        if (decltype(two)::value == 2) acc[1][f] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wc, xa[q][1], acc[1][f], 0, 0, 0);
         if (f < 11) wc = unpack16(wfr[f + 1]);
         if (more) wfr[f] = wfrag(rn, f);
         if (f == 0) {  // weight k-step s + 3 (past the unit's end: the next unit's 0, 1, 2)
@@ -367,8 +497,8 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
         }
       }
     };
-    if (tv[1]) kloop(std::true_type{});
-    else kloop(std::false_type{});
+    if (nt == 2) kloop(std::integral_constant<int, 2>{});
+    else kloop(std::integral_constant<int, 1>{});  // (a third, MFMA-free variant for nt == 0 spills)
     cur = nxt;
     unit_src(j + 2, nxt);
     sp.mark(9);
@@ -378,7 +508,7 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
     h8 qh[TPW][2], ql[TPW][2];
 #pragma unroll
     for (int tt = 0; tt < TPW; ++tt) {
-      const int row = 16 * (wr + FW * tt) + fr;  // token / key row of the images
+      const int row = 16 * (2 * wr + tt) + fr;  // token / key row of the images
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
         float x[16];
@@ -406,10 +536,10 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
             *reinterpret_cast<h8*>(kv + IMGF + koff(row, 2 * fq)) = lo0;
             *reinterpret_cast<h8*>(kv + IMGF + koff(row, 2 * fq + 1)) = lo1;
           } else {
-            *reinterpret_cast<h8*>(kv + 2 * IMGF + voff(row, 32 * fq)) = hi0;
-            *reinterpret_cast<h8*>(kv + 2 * IMGF + voff(row, 32 * fq + 16)) = hi1;
-            *reinterpret_cast<h8*>(kv + 3 * IMGF + voff(row, 32 * fq)) = lo0;
-            *reinterpret_cast<h8*>(kv + 3 * IMGF + voff(row, 32 * fq + 16)) = lo1;
+            *reinterpret_cast<h8*>(kv + 2 * IMGF + v32off(row, 32 * fq)) = hi0;
+            *reinterpret_cast<h8*>(kv + 2 * IMGF + v32off(row, 32 * fq + 16)) = hi1;
+            *reinterpret_cast<h8*>(kv + 3 * IMGF + v32off(row, 32 * fq)) = lo0;
+            *reinterpret_cast<h8*>(kv + 3 * IMGF + v32off(row, 32 * fq + 16)) = lo1;
           }
         }
       }
@@ -421,29 +551,70 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
     sp.mark(9);
 
     // ---- 3. attention over the resident K / V ------------------------------------------------------
-    float m[TPW], l[TPW];
-    f4 o[TPW][4];
+    // q as the 32-query tile's B operands: lane group G (tile G & 1, dims 32 (G >> 1) .. + 31) takes the
+    // 16 dims it lacks from group G ^ 1 (permlane16 swap: even groups trade their tile-1 words, odd groups
+    // their tile-0 words); q32h[c] = dims 32 h + 8 c .. + 7
+    h8 q32h[4], q32l[4];
+    {
+      auto xch = [&](const h8& t0, const h8& t1, h8& first, h8& second) __attribute__((always_inline)) {
+        const u4 x = __builtin_bit_cast(u4, t0), y = __builtin_bit_cast(u4, t1);
+        u4 f, g;
 #pragma unroll
-    for (int tt = 0; tt < TPW; ++tt) {
-      m[tt] = -INFINITY;
-      l[tt] = 0.f;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) o[tt][dt] = f4{0.f, 0.f, 0.f, 0.f};
+        for (int d = 0; d < 4; ++d) {
+          const auto w = __builtin_amdgcn_permlane16_swap(x[d], y[d], false, false);
+          f[d] = w[0];
+          g[d] = w[1];
+        }
+        first = __builtin_bit_cast(h8, f);
+        second = __builtin_bit_cast(h8, g);
+      };
+      xch(qh[0][0], qh[1][0], q32h[0], q32h[2]);
+      xch(qh[0][1], qh[1][1], q32h[1], q32h[3]);
+      xch(ql[0][0], ql[1][0], q32l[0], q32l[2]);
+      xch(ql[0][1], ql[1][1], q32l[1], q32l[3]);
     }
+    float m = -1073741824.f, l = 0.f;  // running max (log2 units, an integer), sum
+    f16x o[2] = {};
     const int nkb = (N + KB - 1) / KB;
-    // full key blocks, then the last (masked when N % 32 != 0); one straight-line body per tile count
-    const int nfull = N / KB;
-    auto attend_all = [&](auto ntv) __attribute__((always_inline)) {
-      constexpr int NTV = decltype(ntv)::value;
-      for (int kb = 0; kb < nfull; ++kb)
-        attend_f<NTV, false>(kv + kb * KB * 128, qh, ql, m, l, o, koffs, voffs, kb * KB + 4 * fq, N, sl2);
-      if (nfull < nkb)
-        attend_f<NTV, true>(kv + nfull * KB * 128, qh, ql, m, l, o, koffs, voffs, nfull * KB + 4 * fq, N, sl2);
-    };
-    if (nt == 2) attend_all(std::integral_constant<int, 2>{});
-    else if (nt == 1) attend_all(std::integral_constant<int, 1>{});
+    const int nfull = N / KB;  // full key blocks, then the last (masked when N % 32 != 0)
+    // software-pipelined: block kb + 1's scores are issued before block kb's softmax, so the matrix core
+    // runs them while this wave's softmax issues
+    // With 7 key blocks (N 193 .. 224: ViT @ 224, N = 197) the block loop is straight-line code and every
+    // LDS offset an immediate; otherwise two blocks per iteration with ping-pong score registers (no copy of
+    // the loop-carried scores).
+    if (nt > 0) {
+      auto last = [&](int kb, const f16x& sc) __attribute__((always_inline)) {
+        if (nfull < nkb) softmax_pv32<true>(kv + kb * KB * 128, sc, m, l, o, voffs, kb * KB, N, sl2);
+        else softmax_pv32<false>(kv + kb * KB * 128, sc, m, l, o, voffs, kb * KB, N, sl2);
+      };
+      f16x sa = scores32(kv, q32h, q32l, koffs);
+      if (nkb == 7) {
+#pragma unroll
+        for (int kb = 0; kb < 6; ++kb) {
+          const f16x sb = scores32(kv + (kb + 1) * KB * 128, q32h, q32l, koffs);
+          softmax_pv32<false>(kv + kb * KB * 128, sa, m, l, o, voffs, kb * KB, N, sl2);
+          sa = sb;
+        }
+        last(6, sa);
+      } else {
+        int kb = 0;
+        for (; kb + 2 < nkb; kb += 2) {
+          const f16x sb = scores32(kv + (kb + 1) * KB * 128, q32h, q32l, koffs);
+          softmax_pv32<false>(kv + kb * KB * 128, sa, m, l, o, voffs, kb * KB, N, sl2);
+          sa = scores32(kv + (kb + 2) * KB * 128, q32h, q32l, koffs);
+          softmax_pv32<false>(kv + (kb + 1) * KB * 128, sb, m, l, o, voffs, (kb + 1) * KB, N, sl2);
+        }
+        if (kb + 1 < nkb) {
+          const f16x sb = scores32(kv + (kb + 1) * KB * 128, q32h, q32l, koffs);
+          softmax_pv32<false>(kv + kb * KB * 128, sa, m, l, o, voffs, kb * KB, N, sl2);
+          last(kb + 1, sb);
+        } else {
+          last(kb, sa);
+        }
+      }
+    }
     sp.mark(0);
-    attend_store<OUT, TPW>(tv, l, o, wr, FW, 0, N, b, h, in_scale, out, ldo, qp, tb, st16);
+    attend_store32<OUT>(tv, l, o, wr, N, b, h, in_scale, out, ldo, qp, tb, st16);
     sp.mark(4);
   }
   sp.flush();
