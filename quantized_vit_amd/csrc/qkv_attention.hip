@@ -141,12 +141,15 @@ QVIT_DEV f16x scores32(const int8_t* st, const h8 (&qh)[4], const h8 (&ql)[4], c
 template <bool MASK>
 QVIT_DEV void softmax_pv32(const int8_t* st, const f16x& s, float& m, float& l, f16x (&o)[2],
                            const int (&voffs)[2], int kbase, int N, float sl2) {
+  // the last block's keys 16 .. 31 all past N (N % 32 in 1 .. 16): their P are 0, skip their V reads and P.V
+  const bool half = MASK && kbase + 16 >= N;
   // V fragments of the block issued before the softmax (they land while it runs)
   h8 vh[2][2], vl[2][2];
 #pragma unroll
   for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
     for (int kc = 0; kc < 2; ++kc) {
+      if (kc == 1 && half) continue;  // wave-uniform
       const int o0 = voffs[dt] + 16 * kc * 128;  // voffs includes the V hi image's 2 IMGF
       vh[dt][kc] = join(tr_read(st, o0), tr_read(st, o0 + 8 * 128));
       vl[dt][kc] = join(tr_read(st + IMGF, o0), tr_read(st + IMGF, o0 + 8 * 128));
@@ -191,9 +194,11 @@ QVIT_DEV void softmax_pv32(const int8_t* st, const f16x& s, float& m, float& l, 
   split8_mix(x[0], ph[0], pl[0]);
   split8_mix(x[1], ph[1], pl[1]);
 #pragma unroll
-  for (int kc = 0; kc < 2; ++kc)
+  for (int kc = 0; kc < 2; ++kc) {
+    if (kc == 1 && half) continue;
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt) o[dt] = mfma3w(vh[dt][kc], vl[dt][kc], ph[kc], pl[kc], o[dt]);
+  }
 }
 
 // Normalise and write the wave's 32 queries: fp32 rows, or the next layer's int8 codes. o[dt][4 g + j] is dim
