@@ -285,10 +285,15 @@ def _split_path(dev, B, N, H, A, packed, npad, kpad, bias_pad, da, dw, s, out, m
     return out.cpu()
 
 
-# K != 768 runs the runtime-K projection loop (NKC = 0), K = 768 the unrolled one
+# K != 768 runs the runtime-K projection loop (NKC = 0), K = 768 the unrolled one. N covers the key-block
+# paths of the 32x32 attention: 7 blocks straight-line (193 .. 208; 193 leaves one valid key in the last
+# block), the two-blocks-per-iteration loop with an even / odd block count, a last block masked with its
+# second 16 keys all past N (N % 32 in 1 .. 16: 1, 100, 130, 193, 208) or not (17, 50), and unmasked (N a
+# multiple of 32: 64, 96, 160)
 @pytest.mark.parametrize("B,N,H,K", [(3, 197, 12, 768), (2, 50, 4, 768), (1, 208, 2, 768), (5, 1, 3, 768),
                                      (2, 17, 12, 768), (9, 100, 1, 768), (3, 197, 8, 512), (2, 197, 12, 1024),
-                                     (40, 197, 3, 256)])
+                                     (40, 197, 3, 256), (2, 64, 3, 768), (1, 96, 5, 768), (2, 160, 2, 768),
+                                     (2, 130, 3, 768), (2, 193, 4, 768)])
 def test_qkv_attention_fused_f32_vs_split_path(dev, B, N, H, K):
     A, packed, npad, kpad, bias_pad, da, dw = _fused_case(dev, B, N, H, seed=B * 1000 + N + H, K=K)
     ref = _split_path(dev, B, N, H, A, packed, npad, kpad, bias_pad, da, dw, 2.0 ** -2,
@@ -302,7 +307,7 @@ def test_qkv_attention_fused_f32_vs_split_path(dev, B, N, H, K):
     assert err <= 2e-6 * ref.abs().max().item(), err
 
 
-@pytest.mark.parametrize("B,N,H", [(4, 197, 12), (3, 64, 6)])
+@pytest.mark.parametrize("B,N,H", [(4, 197, 12), (3, 64, 6), (2, 208, 4), (3, 17, 5)])
 def test_qkv_attention_fused_int8_codes(dev, B, N, H):
     from quantized_vit_amd.quant_layers import epilogue_table_geometry, saturation_level
     A, packed, npad, kpad, bias_pad, da, dw = _fused_case(dev, B, N, H, seed=7 + N)
