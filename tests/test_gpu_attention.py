@@ -329,6 +329,39 @@ def test_qkv_attention_fused_int8_codes(dev, B, N, H):
     assert len(torch.unique(ref)) > 60
 
 
+# the output epilogue's other paths: the per-element quantizer (no code table) and rows whose stride is not a
+# multiple of 16 B (4-B stores instead of the permlane32-paired 16-B ones); the output is a column view of a
+# wider buffer, whose pad columns must stay untouched
+@pytest.mark.parametrize("use_table,pad", [(False, 0), (True, 4), (False, 4)])
+def test_qkv_attention_fused_int8_store_paths(dev, use_table, pad):
+    from quantized_vit_amd.quant_layers import epilogue_table_geometry, saturation_level
+    B, N, H = 3, 197, 4
+    C = 64 * H
+    A, packed, npad, kpad, bias_pad, da, dw = _fused_case(dev, B, N, H, seed=11 + pad)
+    qm, t = 0.5, 0.9
+    d = qm ** t / 127
+    kw = dict(out_qtype=_lib.QT_NONLINEAR, out_d=_p(d, dev), out_qm=_p(qm, dev), out_t=_p(t, dev))
+    table = None
+    if use_table:
+        geo = epilogue_table_geometry(_lib.QT_NONLINEAR, d, qm, t, saturation_level(_lib.QT_NONLINEAR, d, qm, t),
+                                      False)
+        table = _lib.epi_table_build(_lib.EPI_I8, _lib.QT_NONLINEAR, kw["out_d"], kw["out_qm"], kw["out_t"], 0, *geo,
+                                     dev)
+    ref = _split_path(dev, B, N, H, A, packed, npad, kpad, bias_pad, da, dw, 1.0,
+                      torch.zeros((B * N, C), dtype=torch.int8, device=dev), _lib.ATT_I8, epi_table=table, **kw)
+    big = torch.full((B * N, C + pad), 99, dtype=torch.int8, device=dev)
+    out = big[:, :C]
+    _lib.qkv_attention(A, B, N, kpad, packed, npad, da, dw, bias_pad, H, 0.125, out, _lib.ATT_I8, 1.0,
+                       epi_table=table, **kw)
+    torch.cuda.synchronize()
+    diff = (out.cpu().to(torch.int32) - ref.to(torch.int32)).abs()
+    assert diff.max().item() <= 1
+    assert (diff > 0).float().mean().item() <= 1e-3
+    assert len(torch.unique(ref)) > 60
+    if pad:
+        assert (big[:, C:].cpu() == 99).all()
+
+
 def test_qkv_attention_argument_validation(dev):
     lib = _lib.load()
     s = torch.cuda.current_stream().cuda_stream
