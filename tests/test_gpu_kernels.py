@@ -254,8 +254,12 @@ def test_pack_weight_overflow_flag(dev):
     assert ovf.item() == 0
 
 
+# patch embeddings (k = s: 16 @224 and @384, 8 with 4 trailing pixels past the last patch, 4) and padded /
+# strided / 1x1 convolutions
 @pytest.mark.parametrize("conv", [dict(k=16, s=16, p=0, C=3, H=224), dict(k=3, s=1, p=1, C=16, H=20),
-                                  dict(k=3, s=2, p=1, C=5, H=17), dict(k=1, s=1, p=0, C=64, H=13)])
+                                  dict(k=3, s=2, p=1, C=5, H=17), dict(k=1, s=1, p=0, C=64, H=13),
+                                  dict(k=16, s=16, p=0, C=3, H=384), dict(k=8, s=8, p=0, C=2, H=44),
+                                  dict(k=4, s=4, p=0, C=8, H=20)])
 def test_im2col_quant_vs_oracle(dev, conv):
     g = torch.Generator().manual_seed(6)
     B = 2
