@@ -249,10 +249,6 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   const int hi = lo + per + (xcd < rem ? 1 : 0);
   int t = lo + slot;
   if (t >= hi) return;
-#if defined(QVIT_GEMM_STAGGER)
-  if (blockIdx.x >= (gridDim.x >> 1))
-    for (int i = 0; i < QVIT_GEMM_STAGGER; ++i) __builtin_amdgcn_s_sleep(64);
-#endif
 
   // epilogue scalars and the code table are set up before the main loop
   // W4 accumulators hold 16 acc exactly: the float epilogues fold the 1/16 into alpha, which gives the very
