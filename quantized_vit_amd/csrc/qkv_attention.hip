@@ -172,7 +172,7 @@ QVIT_DEV void softmax_pv32(const int8_t* st, const f16x& s, float& m, float& l, 
   // SLP-packed into v_pk_mul_f32 (packed f32 VALU beside the MFMAs costs several times its issue slot)
   if (__builtin_amdgcn_ballot_w64(bm > m + 8.f) != 0) {
     const float mn = __builtin_ceilf(fmax_nn(m, bm));
-    const int k = (int)fmax_nn(m - mn, -256.f);  // m starts at -2^30: the first block scales 0 by 2^-256
+    const int k = (int)fmax_nn(m - mn, -256.f);  // the first block (m = -inf) scales the zero o, l by 2^-256
     l = __builtin_amdgcn_ldexpf(l, k);
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
@@ -578,7 +578,7 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
       xch(ql[0][0], ql[1][0], q32l[0], q32l[2]);
       xch(ql[0][1], ql[1][1], q32l[1], q32l[3]);
     }
-    float m = -1073741824.f, l = 0.f;  // running max (log2 units, an integer), sum
+    float m = -INFINITY, l = 0.f;  // running max (log2 units; an integer once set), sum
     f16x o[2] = {};
     const int nkb = (N + KB - 1) / KB;
     const int nfull = N / KB;  // full key blocks, then the last (masked when N % 32 != 0)

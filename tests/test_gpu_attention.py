@@ -329,6 +329,29 @@ def test_qkv_attention_fused_int8_codes(dev, B, N, H):
     assert len(torch.unique(ref)) > 60
 
 
+# known answer: zero weights, q bias -30, k bias +30, so every score of a row is the same large negative
+# number (-1.04e4 in log2 units after scaling) and the softmax is uniform: out = v's bias on every row (the f32
+# output undoes in_scale), exact up to the fp16 hi/lo operand split
+def test_qkv_attention_fused_uniform_rows(dev):
+    from test_gpu_kernels import pack_codes
+    B, N, H, K = 2, 197, 2, 768
+    C = 64 * H
+    A, _, _, kpad, _, da, dw = _fused_case(dev, B, N, H, seed=5)
+    packed, npad, kpad2 = pack_codes(torch.zeros(3 * C, K, dtype=torch.int64), _lib.W4, dev)
+    assert kpad2 == kpad
+    g = torch.Generator().manual_seed(9)
+    vb = torch.randn(C, generator=g)
+    bias = torch.cat([torch.full((C,), -30.0), torch.full((C,), 30.0), vb])
+    bias_pad = _lib.pad_bias(bias.to(dev), 3 * C, npad, dev)
+    out = torch.full((B * N, C), float("nan"), device=dev)
+    _lib.qkv_attention(A, B, N, kpad, packed, npad, da, dw, bias_pad, H, 0.125, out, _lib.ATT_F32, 2.0 ** -2)
+    torch.cuda.synchronize()
+    got = out.cpu()
+    assert torch.isfinite(got).all()
+    ref = vb.expand(B * N, C)
+    assert (got - ref).abs().max().item() <= 4e-6 * ref.abs().max().item()
+
+
 # the output epilogue's other paths: the per-element quantizer (no code table) and rows whose stride is not a
 # multiple of 16 B (4-B stores instead of the permlane32-paired 16-B ones); the output is a column view of a
 # wider buffer, whose pad columns must stay untouched
