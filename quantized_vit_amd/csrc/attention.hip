@@ -408,12 +408,4 @@ extern "C" int qvit_attention_split(const void* qkv_hi, const void* qkv_lo, int6
   return qvit_hip_status(hipGetLastError());
 }
 
-#ifdef QVIT_ATT_STAMPS
-extern "C" int qvit_att_stamps(unsigned long long* host8, int reset) {
-  if (reset) {
-    const unsigned long long z[16] = {};
-    return qvit_hip_status(hipMemcpyToSymbol(HIP_SYMBOL(qvit_att_stamp_sums), z, sizeof(z)));
-  }
-  return qvit_hip_status(hipMemcpyFromSymbol(host8, HIP_SYMBOL(qvit_att_stamp_sums), 16 * sizeof(unsigned long long)));
-}
-#endif
+QVIT_ATT_STAMP_READER(qvit_att_stamps)  // diag_stamps.h: -DQVIT_ATT_STAMPS builds only

@@ -1,6 +1,7 @@
 // Shared pieces of the attention kernels (attention.hip, qkv_attention.hip): fp16 hi/lo operand
 // images, the 3-pass fp16 MFMA product, the online-softmax block update and the output epilogue.
 #pragma once
+#include "diag_stamps.h"
 #include "qvit_common.h"
 
 namespace qvit_attn {
@@ -69,32 +70,7 @@ QVIT_DEV float xsum(float v) {
 #define QVIT_ATT_DEFER 1
 #endif
 
-// Diagnostic build only (-DQVIT_ATT_STAMPS, tools/attn_bench.py --stamps): per-phase s_memtime sums
-// (0 block wait + DMA issue, 1 scores, 2 softmax, 3 PV, 4 epilogue, 5 query-block reads).
-
-#ifdef QVIT_ATT_STAMPS
-static __device__ unsigned long long qvit_att_stamp_sums[16];
-struct Stamps {
-  unsigned long long a[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long prev = __builtin_amdgcn_s_memtime();
-  QVIT_DEV void mark(int i) {
-    const unsigned long long t = __builtin_amdgcn_s_memtime();
-    a[i] += t - prev;
-    prev = t;
-  }
-  QVIT_DEV void flush() {
-    if ((threadIdx.x & 63) == 0) {
-      for (int i = 0; i < 10; ++i) atomicAdd(&qvit_att_stamp_sums[i], a[i]);
-      atomicAdd(&qvit_att_stamp_sums[15], 1ull);
-    }
-  }
-};
-#else
-struct Stamps {
-  QVIT_DEV void mark(int) {}
-  QVIT_DEV void flush() {}
-};
-#endif
+// Stamps (phase timing of diagnostic builds; empty in the library): diag_stamps.h.
 
 // Online-softmax update of one key block (KB keys in the LDS images at st) for a wave's first NT query
 // tiles, in three phases that keep the live fragments small (2 waves per SIMD leave 256 registers):

@@ -26,6 +26,7 @@
 #include <cstddef>
 #include <type_traits>
 
+#include "diag_stamps.h"
 #include "qvit_common.h"
 
 namespace {
@@ -176,35 +177,6 @@ __global__ void epi_table_kernel(int gelu, int out_qtype, const float* out_d, co
   if (!ok) atomicAnd(&hdr->valid, 0);
 }
 
-// Diagnostic build only (-DQVIT_GEMM_STAMPS, tools/gemm_stamps.py): per-phase s_memtime cycle sums.
-// In the product library these macros are empty.
-#ifdef QVIT_GEMM_STAMPS
-__device__ unsigned long long qvit_gemm_stamp_sums[8];
-#define QVIT_STAMP_DECL                                 \
-  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0};   \
-  unsigned long long st_prev = __builtin_amdgcn_s_memtime();
-#define QVIT_STAMP(i)                                          \
-  do {                                                         \
-    const unsigned long long st_t = __builtin_amdgcn_s_memtime(); \
-    st_acc[i] += st_t - st_prev;                               \
-    st_prev = st_t;                                            \
-  } while (0)
-#define QVIT_STAMP_FLUSH                                                   \
-  do {                                                                     \
-    if (lane == 0) {                                                       \
-      for (int st_i = 0; st_i < 6; ++st_i) atomicAdd(&qvit_gemm_stamp_sums[st_i], st_acc[st_i]); \
-      atomicAdd(&qvit_gemm_stamp_sums[7], 1ull);                           \
-    }                                                                      \
-  } while (0)
-#else
-#define QVIT_STAMP_DECL
-#define QVIT_STAMP(i) \
-  do {                \
-  } while (0)
-#define QVIT_STAMP_FLUSH \
-  do {                   \
-  } while (0)
-#endif
 
 template <int WFMT>
 struct Frags {
@@ -837,17 +809,7 @@ extern "C" int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda, con
   return dispatch_epi<QVIT_W8>(epilogue, A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
 }
 
-#ifdef QVIT_GEMM_STAMPS
-// Diagnostic entry points (not part of include/qvit_hip.h): phase sums
-// [0 prologue, 1 DMA issue, 2 stage wait, 3 fragment reads + MFMA issue, 4 epilogue, 5 step-top drain, 7 waves].
-extern "C" int qvit_gemm_stamps(unsigned long long* host8, int reset) {
-  if (reset) {
-    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    return qvit_hip_status(hipMemcpyToSymbol(HIP_SYMBOL(qvit_gemm_stamp_sums), z, sizeof(z)));
-  }
-  return qvit_hip_status(hipMemcpyFromSymbol(host8, HIP_SYMBOL(qvit_gemm_stamp_sums), 8 * sizeof(unsigned long long)));
-}
-#endif
+QVIT_GEMM_STAMP_READER  // diag_stamps.h: exists only in -DQVIT_GEMM_STAMPS builds
 
 extern "C" int qvit_gemm_qkv_split(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int wfmt,
                                    int64_t N, int64_t npad, const float* d_act, const float* d_wt, const float* bias,

@@ -677,13 +677,4 @@ extern "C" int qvit_qkv_attention(const int8_t* A, int64_t B, int64_t N, int64_t
   return qvit_hip_status(hipGetLastError());
 }
 
-#ifdef QVIT_ATT_STAMPS
-extern "C" int qvit_qkv_att_stamps(unsigned long long* host8, int reset) {
-  if (reset) {
-    const unsigned long long z[16] = {};
-    return qvit_hip_status(hipMemcpyToSymbol(HIP_SYMBOL(qvit_attn::qvit_att_stamp_sums), z, sizeof(z)));
-  }
-  return qvit_hip_status(
-      hipMemcpyFromSymbol(host8, HIP_SYMBOL(qvit_attn::qvit_att_stamp_sums), 16 * sizeof(unsigned long long)));
-}
-#endif
+QVIT_ATT_STAMP_READER(qvit_qkv_att_stamps)  // diag_stamps.h: -DQVIT_ATT_STAMPS builds only
