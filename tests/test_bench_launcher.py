@@ -39,3 +39,16 @@ def test_bench_world_size_mismatch_is_an_error():
              extra_env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0
     assert "WORLD_SIZE" in (r.stderr + r.stdout)
+
+
+def test_metric_names_the_workload_run():
+    """The headline workload carries BASELINE.json's metric verbatim; any other workload names itself."""
+    import json
+    import os
+    import bench
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "BASELINE.json")) as f:
+        base = json.load(f)
+    assert bench.metric_for("vit_base_patch16_224", 224, 256) == bench.METRIC == base["metric"]
+    m = bench.metric_for("vit_large_patch16_384", 384, 128)
+    assert "vit_large_patch16_384" in m and "batch 128" in m and m != bench.METRIC
