@@ -300,7 +300,10 @@ QVIT_DEV float wave_sum_fast(float v) {
 // rows wave, wave + nwaves, ... with the next row's load in flight while the current row is finished;
 // gamma/beta, the quantizer scalars and the code table (QVIT_EPI_I8 semantics, nullable) are read once
 // per workgroup. Same arithmetic as layernorm_quant_reg_kernel, row for row.
-constexpr int LN_TBL_BYTES = 16384;
+#ifndef QVIT_LN_TBL_BYTES
+#define QVIT_LN_TBL_BYTES 16384
+#endif
+constexpr int LN_TBL_BYTES = QVIT_LN_TBL_BYTES;
 #ifndef QVIT_LN_MINW
 #define QVIT_LN_MINW 1
 #endif
