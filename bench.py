@@ -63,6 +63,7 @@ INT8_PEAK_TOPS = 256 * 4 * 2048 * 2.4e9 / 1e12
 FP16_PEAK_TFLOPS = INT8_PEAK_TOPS / 2
 HBM_PEAK_GBS = 8000.0
 DRYRUN = os.environ.get("QVIT_BENCH_DRYRUN") == "1"
+ONE_DEVICE = os.environ.get("QVIT_BENCH_ONE_DEVICE") == "1"
 
 
 def parse(argv=None):
@@ -186,9 +187,14 @@ def tie_resolved_parity(model, model_name: str, img_size: int, dev) -> dict:
                       depth=mc["depth"], num_heads=mc["num_heads"])
     load_oracle_weight_codes(model, cfg)
     r = tie_resolved_vit_check(model, cfg, synthetic_images(2, img_size, seed=12345), dev)
-    return {"rel": r["rel"], "tie_flips": r["flips"], "codes": r["codes"],
-            "non_tie_differences": sum(s.get("non_ties", 0) for s in r["stats"].values()),
-            "batch": 2, "bound": "north star 1e-3 on identical int4 weights"}
+    non_ties = sum(s.get("non_ties", 0) for s in r["stats"].values())
+    missing, bad = list(r["missing"]), list(r["bad"])
+    return {"rel": r["rel"], "tie_flips": r["flips"], "codes": r["codes"], "non_tie_differences": non_ties,
+            "missing_layers": missing, "bad_layers": bad,
+            "pass": bool(not missing and not bad and non_ties == 0 and r["rel"] <= 1e-3),
+            "batch": 2, "bound": "north star 1e-3 on identical int4 weights",
+            "weights": "the oracle's weight codes bound to the model after the timed region (the timed steps ran "
+                       "the device-derived codes; test_device_weight_codes_vs_reference pins those per code)"}
 
 
 def model_gemm_ops(model, B: int) -> float:
@@ -238,6 +244,10 @@ def load_profile_json(name: str, model_name: str, B: int):
         return None
     if j.get("batch") != B or j.get("model") != model_name:
         return None
+    # counters measured on another build of the library are not this line's numbers
+    from quantized_vit_amd import _lib
+    if j.get("lib_build_id") is None or j.get("lib_build_id") != _lib.build_id():
+        return None
     return j
 
 
@@ -258,8 +268,15 @@ def main():
 
     from quantized_vit_amd import _lib, build as qbuild, vit_model
     from quantized_vit_amd.calibrate import build_quantized_vit, synthetic_images
+    # QVIT_BENCH_ONE_DEVICE=1 (tests/test_gpu_bench_ranks.py): every rank on cuda:0 and the gloo backend
+    # (RCCL needs one GPU per rank), so this N-rank branch runs end to end on a one-GPU box; the logits are
+    # staged through the host only for gloo (distributed.gather_logits)
+    one_device = ONE_DEVICE and world > 1
+    backend = "gloo" if one_device else "nccl"
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group(backend, init_method="env://")
+    if one_device:
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if rank == 0:
@@ -305,9 +322,17 @@ def main():
         torch.cuda.synchronize()
         for n in names[1:]:
             events[n] = vit_model.KERNEL_TIMING.pop(n)
+        gather_ok = None
+        if world > 1:   # untimed: the gathered rows of this rank are exactly its own forward
+            from quantized_vit_amd.distributed import shard_bounds
+            s, e = shard_bounds(global_batch, world, rank)
+            ok = torch.tensor([1 if torch.equal(step()[s:e], model(x)) else 0], dtype=torch.int32,
+                              device="cpu" if backend == "gloo" else dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            gather_ok = bool(ok.item())
     launch_ms = {n: (sum(s.elapsed_time(e) for s, e in ev) / len(ev)) if ev else None for n, ev in events.items()}
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if backend == "gloo" else dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
@@ -361,18 +386,25 @@ def main():
         "config": {"workload": f"{args.model} int4w/int8a forward, batch {B} per GPU"
                                + (", RCCL all-gather of logits" if world > 1 else ""),
                    "model": args.model, "global_batch": global_batch, "seq_len": model.patch_embed.num_patches + 1,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}"}
+                  | ({"rehearsal": f"{world} ranks on one device, gloo, logits gathered through the host "
+                                   "(QVIT_BENCH_ONE_DEVICE=1; not a scaling measurement)"} if one_device else {}),
         "roofline": {"bound": "mfma", "kernel": "fc1 gemm_kernel<W4, EPI_I8_GELU>",
                      "achieved": achieved, "peak": INT8_PEAK_TOPS, "unit": "TFLOP/s",
                      "frac": achieved / INT8_PEAK_TOPS, "traffic": traffic,
                      "ops_per_launch": ops, "launch_ms": fc1_ms,
                      "mfma_util": (pmc or {}).get("kernels", {}).get("fc1", {}).get("mfma_busy_frac"),
                      "note": "int8 ops (TOPS) counted as 2*M*N*K; mfma_util = SQ_VALU_MFMA_BUSY_CYCLES / "
-                             "(GRBM_GUI_ACTIVE x CUs) from profiles/pmc_mfma.json"},
+                             "(GRBM_GUI_ACTIVE x CUs) from profiles/pmc_mfma.json; traffic from "
+                             "profiles/fc1_traffic.json; both only when measured on this library build "
+                             "(lib_build_id), else null",
+                     "lib_build_id": _lib.build_id()},
         "model_frac": {"int8_ops_per_step": total_ops, "achieved_TOPS": total_ops / (ms_per_step * 1e-3) / 1e12,
                        "frac": total_ops / (ms_per_step * 1e-3) / 1e12 / INT8_PEAK_TOPS},
         "kernels": kernels,
     }
+    if gather_ok is not None:
+        result["gather_check"] = gather_ok
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         def gpu_logits(img):
             return model(img.to(dev)).cpu()

@@ -118,6 +118,18 @@ def version() -> str:
     return load().qvit_version().decode()
 
 
+def build_id(path: Optional[str] = None) -> Optional[str]:
+    """Identity of a library build (sha256 prefix of the .so file): profile JSONs record the build they
+    were measured on, and bench.py merges their counters only into a line timed on that same build."""
+    import hashlib
+    p = path or (getattr(_lib, "_name", None) if _lib is not None else None) or LIB_PATH
+    try:
+        with open(p, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
 def _check(code: int, what: str) -> None:
     if code != 0:
         msg = load().qvit_strerror(code).decode()

@@ -42,23 +42,38 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found: the HIP extension cannot be built")
 
 
-def _newest_input_mtime() -> float:
+def source_digest(defines: tuple = ()) -> str:
+    """sha256 of every input of the build (sources, headers, this script, flags and defines): a library
+    is reused only when the digest recorded beside it matches, never on file times alone."""
+    import hashlib
+    h = hashlib.sha256()
     paths = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
-    paths.append(os.path.join(INCLUDE, "qvit_hip.h"))
-    paths.append(os.path.abspath(__file__))
-    return max(os.path.getmtime(p) for p in paths)
+    paths += [os.path.join(INCLUDE, "qvit_hip.h"), os.path.abspath(__file__)]
+    for p in paths:
+        h.update(os.path.basename(p).encode())
+        with open(p, "rb") as f:
+            h.update(f.read())
+    h.update(" ".join(HIPCC_FLAGS + [f"-D{d}" for d in defines]).encode())
+    return h.hexdigest()
 
 
-def is_stale(lib: str = LIB) -> bool:
-    return not os.path.exists(lib) or os.path.getmtime(lib) < _newest_input_mtime()
+def is_stale(lib: str = LIB, defines: tuple = ()) -> bool:
+    if not os.path.exists(lib):
+        return True
+    try:
+        with open(lib + ".srcsha") as f:
+            return f.read().strip() != source_digest(defines)
+    except OSError:
+        return True
 
 
 def build(force: bool = False, verbose: bool = False, defines: tuple = (), lib: str = LIB,
           build_dir: str = BUILD) -> str:
     """Builds the library. `defines`/`lib`/`build_dir` produce diagnostic variants (e.g. the
     QVIT_GEMM_STAMPS phase-timing build used by tools/gemm_stamps.py) without touching LIB."""
-    if not force and not is_stale(lib):
+    if not force and not is_stale(lib, defines):
         return lib
+    digest = source_digest(defines)
     hipcc = _hipcc()
     os.makedirs(build_dir, exist_ok=True)
     dflags = [f"-D{d}" for d in defines]
@@ -83,6 +98,8 @@ def build(force: bool = False, verbose: bool = False, defines: tuple = (), lib: 
     if res.returncode != 0:
         raise RuntimeError(f"link failed:\n{res.stdout}\n{res.stderr}")
     os.replace(tmp, lib)
+    with open(lib + ".srcsha", "w") as f:
+        f.write(digest + "\n")
     return lib
 
 

@@ -26,6 +26,10 @@ def gather_logits(local: torch.Tensor, global_batch: int, group: Optional[dist.P
     world = dist.get_world_size(group)
     if world == 1:
         return local
+    if local.is_cuda and dist.get_backend(group) == "gloo":
+        # gloo moves host buffers only (the one-device rehearsal of the N-rank path);
+        # RCCL ("nccl") gathers device buffers in place
+        return gather_logits(local.cpu(), global_batch, group).to(local.device)
     per = -(-global_batch // world)
     C = local.shape[1]
     buf = local
@@ -64,7 +68,11 @@ class ShardedInference:
     @torch.no_grad()
     def forward_shard(self, local_images: torch.Tensor, global_batch: int) -> torch.Tensor:
         """This rank's images (already resident on its device, e.g. generated there) -> all logits."""
-        world, _ = self.world_rank()
+        world, rank = self.world_rank()
+        s, e = shard_bounds(global_batch, world, rank)
+        if local_images.shape[0] != e - s:
+            raise ValueError(f"rank {rank} of {world}: shard of {local_images.shape[0]} images, but images "
+                             f"[{s}, {e}) of the global batch {global_batch} belong to it")
         local = self.model(local_images)
         if world == 1:
             return local

@@ -314,7 +314,6 @@ class QuantizeMixin:
             qm_pack, t_pack = torch.full((1,), 1024.0, device=dev), None
         else:
             qt_pack, d_pack, qm_pack, t_pack = qt, d_wt, qm_wt, t_wt
-        plan.extra["w_codes_src"] = (w32, qt_pack, d_pack, qm_pack, t_pack)
         if act_ok and abs(lw) <= 127:
             overflow = torch.zeros(1, dtype=torch.int32, device=dev)
             for wfmt in ((_lib.W4, _lib.W8) if abs(lw) <= 7 else (_lib.W8,)):
@@ -332,13 +331,16 @@ class QuantizeMixin:
             plan.extra["act_host"] = (qt, s[3], s[4], s[5] if t_act is not None else 1.0, la)
         if not plan.int_path:   # weight-only mode, or levels that fit neither int4 nor int8 (e.g. 16/32 bits)
             plan.w_fakequant = self._fake_quant_weight(plan)
-        plan.extra.pop("w_codes_src")
         return plan
 
     def _fake_quant_weight(self, plan: QuantPlan) -> torch.Tensor:
-        src = plan.extra.get("w_codes_src")
-        if src is not None and plan.extra.get("weight_codes"):
-            return (plan.d_wt * src[0]).view_as(self.weight)      # d_w * k, as quantize_weight returns it
+        """quantize_weight(W) on the device; with codes bound by load_weight_codes, d_w * k of exactly those
+        codes (also when the plan is on the int path and the fp32 form is only filled later, e.g. for a
+        grouped conv whose forward takes the library path)."""
+        codes = self._bound_weight_codes(plan.key)
+        if codes is not None:
+            k = codes.to(device=plan.device, dtype=torch.float32)
+            return (plan.d_wt * k).view_as(self.weight)      # d_w * k, as quantize_weight returns it
         return _lib.fake_quant_f32(self.weight.detach().float(), plan.qtype, plan.d_wt, plan.qm_wt, plan.t_wt)
 
     def weight_codes(self) -> torch.Tensor:

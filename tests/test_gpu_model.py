@@ -147,6 +147,27 @@ def test_weight_and_activation_wide_bits_fp_path(dev, bits, qt):
     assert rel(y, ref) < 1e-5 and rel(yc, refc) < 1e-5
 
 
+def test_bound_codes_reach_grouped_conv_library_path(dev):
+    """a conv whose plan is on the int path but whose forward takes the library conv
+    (groups > 1) must run exactly the weight codes bound by load_weight_codes, not re-derived ones."""
+    torch.manual_seed(11)
+    conv = nn.Conv2d(8, 16, 3, stride=1, padding=1, groups=2, bias=True)
+    q = QuantizeConv2d.from_module(conv, quant_type=QuantizationType.SYMMETRIC_NONLINEAR,
+                                   quant_mode=QuantizationMode.WEIGHT_AND_ACTIVATION, num_bits=4).to(dev).eval()
+    with torch.no_grad():
+        q.q_m_act.fill_(1.0)
+        q.d_quant_act.fill_(1.0 / 127)
+    codes = torch.randint(-7, 8, tuple(q.weight.shape), generator=torch.Generator().manual_seed(3))
+    q.load_weight_codes(codes)
+    assert q.quant_plan().int_path and not q._int_conv_ok()
+    x = (torch.rand(2, 8, 12, 12) * 2 - 1).to(dev)
+    with torch.no_grad():
+        y = q(x)
+        ref = F.conv2d(q.quantize_act(x), q.d_quant_wt * codes.float().to(dev), q.bias, 1, 1, 1, 2)
+    assert torch.equal(q.weight_codes().cpu(), codes.reshape(16, -1).float())
+    assert rel(y, ref) < 1e-6
+
+
 def test_plan_cache_tracks_parameter_versions(dev):
     q = _calibrated_linear(dev, 128, 64, QuantizationType.SYMMETRIC_NONLINEAR)
     p1 = q.quant_plan()
@@ -224,6 +245,27 @@ def test_vit_tiny_b8_vs_oracle(dev, t_act):
     model = build_quantized_vit("vit_tiny_patch16_224", seed=3, t_act=t_act).to(dev)
     cfg = O.ViTConfig(embed_dim=192, depth=12, num_heads=3)
     check_vit_parity(model, cfg, synthetic_images(8, 224, seed=0), dev)
+
+
+@pytest.mark.parametrize("qt", [QuantizationType.SYMMETRIC_NONLINEAR, QuantizationType.SYMMETRIC_LINEAR])
+def test_vit_shipping_weight_codes_end_to_end(dev, qt):
+    """The shipped configuration end to end: the device derives its own weight codes (no
+    load_weight_codes), and the logits must sit within 2.5x the reference's own fp32-vs-fp64 distance
+    (+1e-4) of the oracle's fp32 forward on the same images."""
+    model = build_quantized_vit("vit_tiny_patch16_224", seed=8, quant_type=qt).to(dev)
+    cfg = O.ViTConfig(embed_dim=192, depth=12, num_heads=3,
+                      quant_type=O.LINEAR if qt == QuantizationType.SYMMETRIC_LINEAR else O.NONLINEAR)
+    assert all(getattr(m, "_weight_codes", None) is None for m in model.modules())
+    img = synthetic_images(4, 224, seed=3)
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    with torch.no_grad():
+        y = model(img.to(dev))
+        ref32 = O.vit_forward(sd, cfg, img)
+        ref64 = O.vit_forward({k: v.double() for k, v in sd.items()}, cfg, img.double())
+    floor = rel(ref32, ref64)
+    err = rel(y, ref32)
+    print(f"shipping path: rel {err:.3e}, reference fp32-vs-fp64 floor {floor:.3e}")
+    assert err <= 2.5 * floor + 1e-4, (err, floor)
 
 
 def test_vit_linear_quantizer_vs_oracle(dev):

@@ -45,6 +45,17 @@ def pmc_values(d, counter):
     return vals
 
 
+def _build_id():
+    """The profiled library's build id (quantized_vit_amd._lib.build_id; no torch import needed)."""
+    import hashlib
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    try:
+        with open(os.path.join(root, "quantized_vit_amd", "libqvit_hip.so"), "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
 def pmc(fetch_dir, write_dir, rnd):
     fetch = pmc_values(fetch_dir, "FETCH_SIZE")
     write = pmc_values(write_dir, "WRITE_SIZE")
@@ -62,6 +73,7 @@ def pmc(fetch_dir, write_dir, rnd):
         "traffic_bytes_per_launch": f_b + w_b,
         "corrections": "FETCH_SIZE x2 (gfx950 64-B tally of 128-B requests), KB->B x1024; WRITE_SIZE as is",
         "round": rnd,
+        "lib_build_id": _build_id(),
         # the profiled command: bench.py defaults (tools/profile_fc1.sh)
         "batch": int(os.environ.get("BENCH_BATCH", "256")),
         "model": os.environ.get("BENCH_MODEL", "vit_base_patch16_224"),

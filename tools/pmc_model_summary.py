@@ -104,7 +104,10 @@ def main():
             k["lds_conflict_share"] = g("SQ_LDS_BANK_CONFLICT") / g("SQ_LDS_IDX_ACTIVE")
         kernels[name] = k
 
-    out = {"model": a.model, "batch": a.batch, "round": a.round,
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from kstats import _build_id
+    out = {"model": a.model, "batch": a.batch, "round": a.round, "lib_build_id": _build_id(),
            "source": "tools/profile_model_pmc.sh (rocprofv3 --pmc, one counter group per run, kernel-trace only) "
                      "over tools/pmc_model.py",
            "conventions": __doc__.split("Conventions (MI355X_MICROARCH.md): ")[1].strip(),
