@@ -14,7 +14,8 @@ from typing import Optional
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libqvit_hip.so")
+# QVIT_LIB: another build of the library (diagnostic A/B runs of the same tests on one box)
+LIB_PATH = os.environ.get("QVIT_LIB") or os.path.join(_HERE, "libqvit_hip.so")
 
 # ---- constants mirrored from include/qvit_hip.h ---------------------------------------------
 QT_LINEAR = 0

@@ -111,7 +111,10 @@ def test_kat4_integer_deploy_epilogue(dev, pool):
         want = Q.maxpool2(want)
     assert len(np.unique(want)) >= 8                                        # a spread of codes, not all 0 / 15
     xd = torch.from_numpy(x.transpose(1, 2, 0)[None].astype(np.int8)).contiguous().to(dev)
-    wd = torch.from_numpy(wv.transpose(0, 2, 3, 1).reshape(cout, -1).astype(np.int8)).contiguous().to(dev)
+    kpad = (9 * cin + 63) // 64 * 64                                        # K order (ky, kx, c), zero padded
+    wk = np.zeros((cout, kpad), dtype=np.int8)
+    wk[:, :9 * cin] = wv.transpose(0, 2, 3, 1).reshape(cout, -1)
+    wd = torch.from_numpy(wk).to(dev)
     got = _lib.ultra_conv_int(xd, 3, wd, cout, torch.from_numpy(inc).to(dev), torch.from_numpy(bias).to(dev),
                               sbits, 4, pool)
     got = got[0].permute(2, 0, 1).cpu().numpy().astype(np.int64)
