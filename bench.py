@@ -74,7 +74,7 @@ def parse(argv=None):
     ap.add_argument("--batch", type=int, default=256, help="images per GPU")
     ap.add_argument("--model", default="vit_base_patch16_224")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-batch", type=int, default=8)
+    ap.add_argument("--cpu-batch", type=int, default=8, help="CPU baseline sample (images)")
     ap.add_argument("--cpu-iters", type=int, default=3)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--lib", default="", help=argparse.SUPPRESS)  # diagnostic: A/B another build of the library
@@ -285,6 +285,8 @@ def main():
         dist.barrier()
     _lib.load(args.lib) if args.lib else _lib.load()
 
+    if args.model == "ultranet":
+        return ultranet_main(args, world, rank, dev, backend, one_device)
     img_size = {"vit_base_patch16_224": 224, "vit_large_patch16_384": 384, "vit_tiny_patch16_224": 224}[args.model]
     model = build_quantized_vit(args.model, seed=args.seed, device=dev)
     B = args.batch
@@ -413,6 +415,129 @@ def main():
         result["parity_rel_err_vs_oracle"] = rel
         result["parity_oracle_fp32_vs_fp64"] = floor
         result["parity_tie_resolved"] = tie_resolved_parity(model, args.model, img_size, dev)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+ULTRA_LAYERS = [  # (name, cin, cout, input size divisor, pooled): mymodel.py:71-124 at 416 x 416
+    ("ultra_conv0", 3, 16, 1, True), ("ultra_conv1", 16, 32, 2, True), ("ultra_conv2", 32, 64, 4, True),
+    ("ultra_conv3", 64, 64, 8, True), ("ultra_conv4", 64, 64, 16, False), ("ultra_conv5", 64, 64, 16, False),
+    ("ultra_conv6", 64, 64, 16, False), ("ultra_conv7", 64, 64, 16, False)]
+
+
+def ultranet_work(size: int = 416) -> dict:
+    """Algorithmic work per image of each UltraNet launch: conv ops 2 H W cout cin 9; bytes =
+    input read once (fp32 image for layer 0, int8 codes after) + output codes written once (pooled)."""
+    work = {}
+    for name, cin, cout, div, pool in ULTRA_LAYERS:
+        hw = (size // div) ** 2
+        out_hw = hw // 4 if pool else hw
+        in_b = hw * cin * (4 if name == "ultra_conv0" else 1)
+        work[name] = {"ops": 2.0 * hw * cout * cin * 9, "bytes": in_b + out_hw * cout}
+    g = (size // 16) ** 2
+    work["ultra_head"] = {"ops": 2.0 * g * 36 * 64, "bytes": g * 64 + g * 36 * 4 + 2 * 2 * g * 36 * 4}
+    return work
+
+
+def ultranet_main(args, world: int, rank: int, dev, backend: str, one_device: bool) -> None:
+    """BASELINE.json configs[4]: the UltraNetQua W4A4 forward (4-bit quantization/mymodel.py:62-144) at 416 x 416
+    on synthetic k/255 images, batch-sharded like the ViT. roofline: the dominant launch, layer 0 (float image
+    -> conv3x3 + BN + A4 quantizer + max pool -> codes), against HBM (UltraNet is HBM-bound)."""
+    from quantized_vit_amd import _lib, vit_model
+    from quantized_vit_amd.ultranet import random_ultranet, synthetic_images_u8
+    size = 416
+    model = random_ultranet(seed=args.seed, device=dev)
+    B = args.batch
+    x = synthetic_images_u8(B, size, seed=1000 + rank, device=dev)
+    assert model.fused_ok(x)
+    sharded = ShardedInference(lambda im: model(im)[0].flatten(1))
+    global_batch = world * B
+    names = [n for n, *_ in ULTRA_LAYERS] + ["ultra_head"]
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            out = sharded.forward_shard(x, global_batch)
+        torch.cuda.synchronize()
+        assert out.shape[0] == global_batch, out.shape
+        vit_model.KERNEL_TIMING["ultra_conv0"] = []
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            sharded.forward_shard(x, global_batch)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        events = {"ultra_conv0": vit_model.KERNEL_TIMING.pop("ultra_conv0")}
+        for n in names[1:]:
+            vit_model.KERNEL_TIMING[n] = []
+        for _ in range(args.steps):
+            sharded.forward_shard(x, global_batch)
+        torch.cuda.synchronize()
+        for n in names[1:]:
+            events[n] = vit_model.KERNEL_TIMING.pop(n)
+    launch_ms = {n: sum(s.elapsed_time(e) for s, e in ev) / len(ev) for n, ev in events.items() if ev}
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if backend == "gloo" else dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    work = ultranet_work(size)
+    kernels = {}
+    for n, ms in launch_ms.items():
+        w = work[n]
+        kernels[n] = {"launch_us": ms * 1e3, "hbm_GBs_algorithmic": w["bytes"] * B / (ms * 1e-3) / 1e9,
+                      "int8_TOPS": w["ops"] * B / (ms * 1e-3) / 1e12}
+    k0 = kernels["ultra_conv0"]
+    img_bytes = sum(w["bytes"] for w in work.values())
+    img_ops = sum(w["ops"] for w in work.values())
+    value = global_batch * args.steps / elapsed
+    result = {
+        "metric": f"images/sec UltraNet int4 @{size} batch {B}; % HBM roofline",
+        "value": value, "unit": "img/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "int8",
+        "data": f"synthetic k/255 {size}x{size} images; random-init UltraNetQua (BN statistics calibrated on its own "
+                "outputs), W4 weights / A4 activations, fused HIP forward",
+        "config": {"workload": f"UltraNetQua W4A4 forward @{size}, batch {B} per GPU"
+                               + (", RCCL all-gather of the detections" if world > 1 else ""),
+                   "model": "ultranet", "global_batch": global_batch, "img_size": size, "parallelism": f"dp{world}"},
+        "roofline": {"bound": "hbm", "kernel": "ultra_conv0 (layer 0: fp32 image in, pooled codes out)",
+                     "achieved": k0["hbm_GBs_algorithmic"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": k0["hbm_GBs_algorithmic"] / HBM_PEAK_GBS, "traffic": None,
+                     "bytes_per_launch": work["ultra_conv0"]["bytes"] * B, "launch_ms": launch_ms["ultra_conv0"]},
+        "model_frac": {"algorithmic_bytes_per_img": img_bytes, "int8_ops_per_img": img_ops,
+                       "hbm_GBs": img_bytes * value / world / 1e9,
+                       "frac_hbm_peak": img_bytes * value / world / 1e9 / HBM_PEAK_GBS},
+        "kernels": kernels,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import ultranet_oracle as U
+        sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+        img = synthetic_images_u8(args.cpu_batch, size, seed=12345)
+        cores = usable_cores()
+        prev = torch.get_num_threads()
+        torch.set_num_threads(cores["threads"])
+        try:
+            with torch.no_grad():
+                ref, _ = U.ultranet_forward(sd, img)          # warm-up, and the parity reference
+                times = []
+                for _ in range(args.cpu_iters):
+                    t1 = time.perf_counter()
+                    U.ultranet_forward(sd, img)
+                    times.append(time.perf_counter() - t1)
+                gpu = model(img.to(dev))[0].cpu()
+            used = torch.get_num_threads()
+        finally:
+            torch.set_num_threads(prev)
+        med = sorted(times)[len(times) // 2]
+        result["cpu_baseline"] = {
+            "value": img.shape[0] / med, "unit": "img/s", "cores": used, "kind": "port",
+            "sample": f"oracle fp32 fake-quant UltraNetQua forward (oracle/ultranet_oracle.py), batch {img.shape[0]}, "
+                      f"median of {args.cpu_iters} after 1 warm-up ({cpu_model_name()}; {used} intra-op threads)"}
+        result["parity_rel_err_vs_oracle"] = ((gpu.double() - ref.double()).norm() / ref.double().norm()).item()
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

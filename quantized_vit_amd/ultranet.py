@@ -21,6 +21,7 @@ import torch.nn as nn
 
 from . import _lib
 from .quant_ultra import activation_quantize_fn, conv2d_Q_fn
+from .vit_model import _timed   # benchmark event hooks (vit_model.KERNEL_TIMING)
 
 
 def create_grids(self, img_size=416, ng=(13, 13), device="cpu", type=torch.float32):
@@ -164,12 +165,15 @@ class UltraNetQua(nn.Module):
         plan, (hcodes, hbias, hout) = self._plan
         img_size = x.shape[-2:]
         c0, a0, s0, _, _ = plan[0]
-        h = _lib.ultra_conv0(x.contiguous(), c0, a0, s0, A_BIT)
-        for codes, alpha, shift, cout, pool in plan[1:]:
+        with _timed("ultra_conv0"):
+            h = _lib.ultra_conv0(x.contiguous(), c0, a0, s0, A_BIT)
+        for k, (codes, alpha, shift, cout, pool) in enumerate(plan[1:], 1):
             mode = _lib.ULTRA_CODES_POOL if pool else _lib.ULTRA_CODES
-            h = _lib.ultra_conv(h, 3, codes, cout, W_BIT, A_BIT, alpha, shift, mode)
-        head = _lib.ultra_conv(h, 1, hcodes, hout, W_BIT, A_BIT, None, hbias, _lib.ULTRA_F32)
-        io, p = self.yololayer.decode_nhwc(head, img_size)
+            with _timed(f"ultra_conv{k}"):
+                h = _lib.ultra_conv(h, 3, codes, cout, W_BIT, A_BIT, alpha, shift, mode)
+        with _timed("ultra_head"):
+            head = _lib.ultra_conv(h, 1, hcodes, hout, W_BIT, A_BIT, None, hbias, _lib.ULTRA_F32)
+            io, p = self.yololayer.decode_nhwc(head, img_size)
         return io, (p,)   # = torch.cat((io,), 1): the single YOLO layer's output, already a fresh tensor
 
     # ---- reference forward ------------------------------------------------------------------
