@@ -180,6 +180,30 @@ int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda,
               int out_levels, const void* epi_table, hipStream_t stream);
 
 /*
+ * The residual contraction of a transformer block with the next LayerNorm behind it, in one launch:
+ * replaces QuantizeLinear.forward of Attention.proj / Mlp.fc2 (quant_layers.py:495-499) + the residual add of
+ * Block.forward (reference vit_model.py:202-208) + the following norm2 / next block's norm1 (vit_model.py:193,
+ * 206-207) + the next layer's quantize_act (quant_layers.py:356-381), i.e. qvit_gemm(QVIT_EPI_F32_RESID) then
+ * qvit_layernorm_quant_i8 on the same rows, with the same results.
+ *   A .. ldc : as qvit_gemm with QVIT_EPI_F32_RESID (C += d_act d_wt acc + bias); N % 4 == 0, N <= 1024,
+ *              M * ldc * 4 < 2^31.
+ *   gamma, beta, eps, out_* , ln_table : the LayerNorm and the next quantizer, as qvit_layernorm_quant_i8
+ *              (ln_table: its QVIT_EPI_I8 code table, nullable; used if valid and <= 2174 buckets).
+ *   codes    : int8 [M][ldcodes], the LayerNorm codes of the updated rows, columns [N, kpad_codes) zero.
+ *   counters : int32 [ceil(M / 128)] (one per 128-row block), zero when first allocated and
+ *              used by launches of one npad only, one launch at a time (stream order): each launch adds
+ *              npad / 256 to every row block's counter, so the buffer is never reset.
+ * The last of a row block's npad / 256 workgroups runs the LayerNorm of its rows; the residual rows are written
+ * through (sc1) and read back with sc1 loads behind an agent-scope counter.
+ */
+int qvit_gemm_resid_ln(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int wfmt,
+                       int64_t N, int64_t npad, const float* d_act, const float* d_wt, const float* bias,
+                       float* C, int64_t ldc, const float* gamma, const float* beta, float eps,
+                       int out_qtype, const float* out_d, const float* out_qm, const float* out_t,
+                       int out_levels, const void* ln_table, int8_t* codes, int64_t ldcodes,
+                       int64_t kpad_codes, int32_t* counters, hipStream_t stream);
+
+/*
  * Code table for the int8 epilogues (optional `epi_table` of qvit_gemm; 16-byte aligned,
  * QVIT_EPI_TABLE_BYTES(nb) bytes). The output code of QVIT_EPI_I8 / QVIT_EPI_I8_GELU is a piecewise
  * constant function of the pre-activation v = d_act d_wt acc + bias; the table holds it exactly over

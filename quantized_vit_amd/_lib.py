@@ -63,6 +63,8 @@ _SIGNATURES = {
     "qvit_gemm": [_c_p, _i64, _i64, _i64, _c_p, _i32, _i64, _i64, _c_p, _c_p, _c_p, _i32, _c_p, _i64,
                   _i32, _c_p, _c_p, _c_p, _i32, _c_p, _c_p],
     "qvit_epi_table_build": [_i32, _i32, _c_p, _c_p, _c_p, _i32, _f32, _f32, _i64, _c_p, _c_p],
+    "qvit_gemm_resid_ln": [_c_p, _i64, _i64, _i64, _c_p, _i32, _i64, _i64, _c_p, _c_p, _c_p, _c_p, _i64, _c_p, _c_p,
+                           _f32, _i32, _c_p, _c_p, _c_p, _i32, _c_p, _c_p, _i64, _i64, _c_p, _c_p],
     "qvit_ultra_weight_codes": [_c_p, _i64, _i64, _i64, _i32, _c_p, _i64, _i64, _c_p, _c_p, _c_p],
     "qvit_ultra_bn_fold": [_c_p, _c_p, _c_p, _c_p, _f32, _i64, _c_p, _c_p, _c_p],
     "qvit_ultra_conv0": [_c_p, _i64, _i64, _i64, _c_p, _c_p, _c_p, _i32, _c_p, _c_p],
@@ -225,6 +227,36 @@ def gemm(A: torch.Tensor, M: int, K: int, packed: torch.Tensor, wfmt: int, N: in
                             _ptr(bias_pad), epilogue, _ptr(C), C.stride(0), out_qtype, _ptr(out_d), _ptr(out_qm),
                             _ptr(out_t), out_levels, _ptr(epi_table), _stream(A.device)), "qvit_gemm")
     return C
+
+
+_LN_COUNTERS: dict = {}
+
+
+def resid_ln_counters(device: torch.device, rows: int, npad: int) -> torch.Tensor:
+    """Arrival counters of qvit_gemm_resid_ln for `rows` rows: one zero-initialised int32 per 128-row block,
+    one buffer per (device, npad) (each launch adds npad / 256 per block, so a buffer serves one npad)."""
+    key = (str(device), npad)
+    need = (rows + 127) // 128
+    buf = _LN_COUNTERS.get(key)
+    if buf is None or buf.numel() < need:
+        buf = torch.zeros(max(need, 1), dtype=torch.int32, device=device)
+        _LN_COUNTERS[key] = buf
+    return buf
+
+
+def gemm_resid_ln(A: torch.Tensor, M: int, K: int, packed: torch.Tensor, wfmt: int, N: int, npad: int,
+                  d_act, d_wt, bias_pad, C: torch.Tensor, gamma, beta, eps: float, out_qtype: int, out_d, out_qm,
+                  out_t, out_levels: int, ln_table, codes: torch.Tensor, kpad_codes: int) -> torch.Tensor:
+    """C += contraction (QVIT_EPI_F32_RESID), then LayerNorm + quantizer of the updated rows -> codes
+    (qvit_gemm_resid_ln)."""
+    _require_gpu(A, "codes")
+    cnt = resid_ln_counters(A.device, M, npad)
+    _check(load().qvit_gemm_resid_ln(_ptr(A), M, K, A.stride(0), _ptr(packed), wfmt, N, npad, _ptr(d_act),
+                                     _ptr(d_wt), _ptr(bias_pad), _ptr(C), C.stride(0), _ptr(gamma), _ptr(beta), eps,
+                                     out_qtype, _ptr(out_d), _ptr(out_qm), _ptr(out_t), out_levels, _ptr(ln_table),
+                                     _ptr(codes), codes.stride(0), kpad_codes, _ptr(cnt), _stream(A.device)),
+           "qvit_gemm_resid_ln")
+    return codes
 
 
 def epi_table_build(epilogue: int, out_qtype: int, out_d, out_qm, out_t, out_levels: int, v_lo: float, w: float,

@@ -10,13 +10,14 @@
 #include "qvit_common.h"
 
 // ---- persistent GEMM (gemm_w4a8.hip): 0 prologue, 1 DMA issue, 2 stage wait,
-//      3 fragment reads + MFMA issue, 4 epilogue, 5 step-top drain, [7] wave count
+//      3 fragment reads + MFMA issue, 4 epilogue, 5 step-top drain, 6 LayerNorm job
+//      (EPI_RESID_LN), [7] wave count
 #ifdef QVIT_GEMM_STAMPS
 namespace {
 __device__ unsigned long long qvit_gemm_stamp_sums[8];
 }  // namespace
 #define QVIT_STAMP_DECL                               \
-  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}; \
+  unsigned long long st_acc[7] = {0, 0, 0, 0, 0, 0, 0}; \
   unsigned long long st_prev = __builtin_amdgcn_s_memtime();
 #define QVIT_STAMP(i)                                             \
   do {                                                            \
@@ -27,7 +28,7 @@ __device__ unsigned long long qvit_gemm_stamp_sums[8];
 #define QVIT_STAMP_FLUSH                                                                           \
   do {                                                                                             \
     if (lane == 0) {                                                                               \
-      for (int st_i = 0; st_i < 6; ++st_i) atomicAdd(&qvit_gemm_stamp_sums[st_i], st_acc[st_i]); \
+      for (int st_i = 0; st_i < 7; ++st_i) atomicAdd(&qvit_gemm_stamp_sums[st_i], st_acc[st_i]); \
       atomicAdd(&qvit_gemm_stamp_sums[7], 1ull);                                                   \
     }                                                                                              \
   } while (0)

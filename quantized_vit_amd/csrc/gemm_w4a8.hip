@@ -27,11 +27,16 @@
 #include <type_traits>
 
 #include "diag_stamps.h"
+#include "ln_common.h"
 #include "qvit_common.h"
 
 namespace {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
+
+// internal epilogue of qvit_gemm_resid_ln: QVIT_EPI_F32_RESID (stores written through, sc1) and, behind the last
+// of a row block's tiles, LayerNorm + the next layer's activation quantizer of that block's rows
+constexpr int EPI_RESID_LN = 16;
 
 constexpr int BN = 256;    // weight rows per tile
 constexpr int BK = 64;     // k per stage
@@ -105,6 +110,15 @@ struct EpiArgs {
   float inv_seq;        // 1 / seq (row -> image with an exact correction)
   float in_scale;       // QKV_SPLIT: power-of-two operand scale
   _Float16* lo;         // QKV_SPLIT: lo plane (C is the hi plane)
+  // EPI_RESID_LN: LayerNorm (gamma, beta, eps) of the finished rows + the next quantizer -> codes
+  const float* ln_gamma;
+  const float* ln_beta;
+  float ln_eps;
+  const int8_t* ln_table;  // its code table (EPI_I8 semantics), nullable
+  int8_t* ln_codes;
+  int64_t ln_ldc;
+  int ln_kpad;
+  int* ln_cnt;             // arrivals per 128-row block (monotone: npad / 256 per launch)
 };
 
 // ---- code table of the int8 epilogues --------------------------------------------------------------
@@ -184,6 +198,23 @@ struct Frags {
   uint2 w4[4];  // W4: packed 16 nibbles per lane
   v4i w8[4];    // W8: 16 bytes per lane
 };
+
+// Residual rows of EPI_RESID_LN are handed to another workgroup inside the launch (the LayerNorm behind the
+// last tile of a row block): written through with sc1 stores, read back with sc1 loads, the hand-off an agent-scope
+// counter after every storing wave's vmcnt(0) (MI355X_MICROARCH.md, inter-workgroup visibility, Valid forms)
+// (the sc1 store is a compiler-visible buffer store, so the hazard recognizer pads what follows it; C + 4 M ldc
+// < 2^31 bytes, checked by the launcher)
+template <bool SC1>
+QVIT_DEV void st_resid(float* dst, float4 o, const float* C0, int M, int64_t ldc) {
+  if constexpr (SC1) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(C0), (short)0,
+                                                                        (int)((int64_t)M * ldc * 4), 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(f4v{o.x, o.y, o.z, o.w}, r, (int)((dst - C0) * 4), 0, 16);
+  } else {
+    *reinterpret_cast<float4*>(dst) = o;
+  }
+}
 
 // Persistent kernel: gridDim.x = a multiple of 8 (blocks are dispatched round-robin over the 8 XCDs);
 // XCD x's blocks share the contiguous tile range [lo_x, hi_x) (tile_n fastest, so the tiles in flight on
@@ -336,6 +367,111 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     __builtin_amdgcn_sched_barrier(0);
   };
 
+  // ---- EPI_RESID_LN: arrival of this tile at its row block; the last of the block's nb_n tiles runs the
+  // LayerNorm + quantizer of its <= 128 rows (wave w: rows m0 + w + 4 i), reading every column back with sc1
+  // loads (the other tiles were written through by other workgroups, possibly on other XCDs)
+  auto ln_after_tile = [&](int m0) __attribute__((always_inline)) {
+    int* flag = reinterpret_cast<int*>(qp_l);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 residual stores have landed
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    asm volatile("s_barrier" ::: "memory");
+    if (tid == 0) {
+      const int old = __hip_atomic_fetch_add(ep.ln_cnt + m0 / BM, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = (old % nb_n) == nb_n - 1 ? 1 : 0;
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    asm volatile("s_barrier" ::: "memory");
+    if (*flag == 0) return;  // workgroup-uniform
+    // the quantizer's code table -> the epilogue region (its staging is done: every wave passed the barrier)
+    const int8_t* ent = nullptr;
+    float c0 = 0.f, inv_w = 0.f, top = 0.f;
+    QParams qp{};
+    if (ep.ln_table != nullptr) {
+      const EpiTableHdr h = *reinterpret_cast<const EpiTableHdr*>(ep.ln_table);
+      if (h.valid != 0 && h.nb >= 1 && h.nb <= G::TABLE_MAX_NB) {
+        const v4i* src = reinterpret_cast<const v4i*>(ep.ln_table);
+        for (int i = tid; i < (16 + 8 * h.nb + 15) / 16; i += G::NT) reinterpret_cast<v4i*>(epi_lds)[i] = src[i];
+        ent = epi_lds + sizeof(EpiTableHdr);
+        c0 = h.c0;
+        inv_w = h.inv_w;
+        top = epi_top(h.nb);
+      }
+    }
+    if (ent == nullptr) qp = load_qparams(ep.out_qtype, ep.out_d, ep.out_qm, ep.out_t, ep.out_levels);
+    const int ln = lane_opaque();
+    const int cols = N;
+    float4 gam[4], bet[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = 4 * (ln + 64 * i);
+      const bool in = c < cols;
+      gam[i] = (in && ep.ln_gamma) ? *reinterpret_cast<const float4*>(ep.ln_gamma + c) : make_float4(1.f, 1.f, 1.f, 1.f);
+      bet[i] = (in && ep.ln_beta) ? *reinterpret_cast<const float4*>(ep.ln_beta + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    asm volatile("s_barrier" ::: "memory");  // the table is in place
+    // sc1 buffer loads (compiler-tracked) of a row's columns 4 (lane + 64 i) .. + 3; zero past the row; rows past
+    // M read row M - 1. Wave w owns rows m0 + w + 4 i; they are taken 8 at a time with all 8 rows' loads in flight
+    // together (the accumulator registers are free here), so the block's 128 rows cost 4 memory latencies.
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<void*>(static_cast<const void*>(C)), (short)0, (int)((int64_t)M * ldc * 4), 0x00020000);
+    // wave w: rows m0 + w + 4 i (i < 32), three per loop iteration from a 3-deep register ring, each row's loads
+    // issued two rows ahead; the rolled loop keeps the job's code small (an unrolled job thrashed the I-cache)
+    auto job = [&](auto nvc, auto modec) __attribute__((always_inline)) {
+      constexpr int NV = decltype(nvc)::value;
+      constexpr int MODE = decltype(modec)::value;
+      const int rend = (m0 + BM < M ? m0 + BM : M);
+      auto ld = [&](int r, f4v (&t)[NV]) __attribute__((always_inline)) {
+        const int rr = r < M ? r : M - 1;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+          const int c = 4 * (ln + 64 * i);
+          t[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(((int64_t)rr * ldc + (c < cols ? c : 0)) * 4), 0, 16);
+        }
+      };
+      auto row = [&](int r, const f4v (&t)[NV]) __attribute__((always_inline)) {
+        float4 v[NV];
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+          v[i] = (4 * (ln + 64 * i) < cols) ? make_float4(t[i][0], t[i][1], t[i][2], t[i][3])
+                                            : make_float4(0.f, 0.f, 0.f, 0.f);
+        uint32_t word[NV];
+        auto gb = [&](int i, float4& g, float4& bb) {
+          g = gam[i];
+          bb = bet[i];
+        };
+        ln_quant_row<NV, decltype(gb), MODE>(v, ln, cols, ep.ln_eps, gb, ent, c0, inv_w, top, qp, word);
+        if (r < rend) {
+          int8_t* cr = ep.ln_codes + (int64_t)r * ep.ln_ldc;
+#pragma unroll
+          for (int i = 0; i < NV; ++i) {
+            const int c = 4 * (ln + 64 * i);
+            if (c < cols) *reinterpret_cast<uint32_t*>(cr + c) = word[i];
+          }
+          for (int c = cols + ln; c < ep.ln_kpad; c += 64) cr[c] = 0;
+        }
+      };
+      f4v t0[NV], t1[NV], t2[NV];
+      const int r0 = m0 + wave;
+      ld(r0, t0);
+      ld(r0 + 4, t1);
+#pragma unroll 1
+      for (int r = r0; r < rend; r += 12) {
+        ld(r + 8, t2);
+        row(r, t0);
+        ld(r + 12, t0);
+        row(r + 4, t1);
+        ld(r + 16, t1);
+        row(r + 8, t2);
+      }
+    };
+    // (the direct quantizer, for a missing or invalid table, is the rare slow path: one row in flight, NV 4)
+    if (ent == nullptr) job(std::integral_constant<int, 4>{}, std::integral_constant<int, 2>{});
+    else if (cols <= 768) job(std::integral_constant<int, 3>{}, std::integral_constant<int, 1>{});
+    else job(std::integral_constant<int, 4>{}, std::integral_constant<int, 1>{});
+  };
+
   Src cs, ns;
   tile_src(t, cs);
   // prologue: the first tile's stages 0 and 1
@@ -462,7 +598,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
             if (nbase + q < N) dst[q] = (int8_t)((wd[q >> 2] >> (8 * (q & 3))) & 0xff);
         }
       }
-    } else if (EPI == QVIT_EPI_F32_RESID) {
+    } else if (EPI == QVIT_EPI_F32_RESID || EPI == EPI_RESID_LN) {
       // C += alpha acc + bias: 16 rows per pass through the wave's staging area, 16 lanes per 64-column
       // row segment; the residual rows of pass sr + 1 are loaded while pass sr is staged and stored, so
       // the read-modify-write pays one memory latency per tile instead of one per row
@@ -508,7 +644,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
             float4 o = make_float4(alpha * (float)a4[0] + b4.x, alpha * (float)a4[1] + b4.y,
                                    alpha * (float)a4[2] + b4.z, alpha * (float)a4[3] + b4.w);
             o.x += ov[i][0]; o.y += ov[i][1]; o.z += ov[i][2]; o.w += ov[i][3];
-            *reinterpret_cast<float4*>(Cf + (int64_t)m * ldc + n) = o;
+            st_resid<EPI == EPI_RESID_LN>(Cf + (int64_t)m * ldc + n, o, Cf, M, ldc);
           }
         };
         ld(0, ov0);
@@ -550,7 +686,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
             if (nfull) {
               const float4 ov = old[sr & 1][i];
               o.x += ov.x; o.y += ov.y; o.z += ov.z; o.w += ov.w;
-              *reinterpret_cast<float4*>(dst) = o;
+              st_resid<EPI == EPI_RESID_LN>(dst, o, Cf, M, ldc);
             } else {
               const float v[4] = {o.x, o.y, o.z, o.w};
               for (int j = 0; j < 4; ++j)
@@ -687,6 +823,10 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     }
     if (I8OUT) __builtin_amdgcn_s_setprio(0);
     QVIT_STAMP(4);
+    if constexpr (EPI == EPI_RESID_LN) {
+      ln_after_tile(m0);
+      QVIT_STAMP(6);
+    }
     if (!has_next) break;
     t = tnext;
     cs = ns;
@@ -732,8 +872,13 @@ int launch(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, i
     if (grid > need) grid = need;
     if (grid < 8) grid = 8;
     void* Cc = reinterpret_cast<int8_t*>(C) + (EPI == QVIT_EPI_QKV_SPLIT ? 0 : m0 * ldc * esize);
+    EpiArgs epc = ep;
+    if (EPI == EPI_RESID_LN) {  // this chunk's row blocks and code rows
+      epc.ln_cnt = ep.ln_cnt + m0 / G::BM;
+      epc.ln_codes = ep.ln_codes + m0 * ep.ln_ldc;
+    }
     hipLaunchKernelGGL((gemm_kernel<WFMT, EPI, WMV>), dim3((unsigned)grid), dim3(G::NT), 0, stream, A + m0 * lda,
-                       (int)mc, (int)K, lda, reinterpret_cast<const int8_t*>(Wp), (int)N, (int)npad, Cc, ldc, ep);
+                       (int)mc, (int)K, lda, reinterpret_cast<const int8_t*>(Wp), (int)N, (int)npad, Cc, ldc, epc);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return qvit_hip_status(e);
   }
@@ -807,6 +952,34 @@ extern "C" int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda, con
              (i8out ? reinterpret_cast<const int8_t*>(epi_table) : nullptr), 1, 1.f, 1.f, nullptr};
   if (wfmt == QVIT_W4) return dispatch_epi<QVIT_W4>(epilogue, A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
   return dispatch_epi<QVIT_W8>(epilogue, A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
+}
+
+extern "C" int qvit_gemm_resid_ln(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int wfmt,
+                                  int64_t N, int64_t npad, const float* d_act, const float* d_wt, const float* bias,
+                                  float* C, int64_t ldc, const float* gamma, const float* beta, float eps,
+                                  int out_qtype, const float* out_d, const float* out_qm, const float* out_t,
+                                  int out_levels, const void* ln_table, int8_t* codes, int64_t ldcodes,
+                                  int64_t kpad_codes, int32_t* counters, hipStream_t stream) {
+  if (!A || !Wp || !C || !codes || !counters || !d_act || !d_wt) return QVIT_ENULL;
+  if (wfmt != QVIT_W4 && wfmt != QVIT_W8) return QVIT_EINVAL;
+  if (M < 0 || K <= 0 || K % KTILE || lda < K || N <= 0 || N > 1024 || N % 4 || npad < N || npad % BN)
+    return QVIT_EINVAL;
+  if (M > INT32_MAX / 2 || K > (1 << 24) || (wfmt == QVIT_W4 && K > 65536)) return QVIT_EINVAL;
+  if (ldc < N || kpad_codes < N || ldcodes < kpad_codes || M * ldc * 4 > 0x7FFFFFFF) return QVIT_EINVAL;
+  if ((lda % 16) || (((uintptr_t)A) & 15) || (((uintptr_t)Wp) & 15)) return QVIT_EALIGN;
+  if ((ldc % 4) || (((uintptr_t)C) & 15) || (ldcodes % 4) || (((uintptr_t)codes) & 3)) return QVIT_EALIGN;
+  if ((((uintptr_t)counters) & 3) || (bias && (((uintptr_t)bias) & 15))) return QVIT_EALIGN;
+  if ((gamma && (((uintptr_t)gamma) & 15)) || (beta && (((uintptr_t)beta) & 15))) return QVIT_EALIGN;
+  if (ln_table && (((uintptr_t)ln_table) & 15)) return QVIT_EALIGN;
+  const int q = out_qtype & 0xff;
+  if (q != QVIT_QT_LINEAR && q != QVIT_QT_NONLINEAR && q != QVIT_QT_ULTRA_ACT) return QVIT_EINVAL;
+  if (q == QVIT_QT_ULTRA_ACT ? (out_levels < 1 || out_levels > 127) : (!out_d || !out_qm)) return QVIT_EINVAL;
+  if (M == 0) return QVIT_OK;
+  EpiArgs ep{d_act, d_wt, bias, out_qtype, out_d, out_qm, out_t, out_levels, nullptr, 1, 1.f, 1.f, nullptr,
+             gamma, beta, eps, reinterpret_cast<const int8_t*>(ln_table), codes, ldcodes, (int)kpad_codes,
+             reinterpret_cast<int*>(counters)};
+  if (wfmt == QVIT_W4) return launch<QVIT_W4, EPI_RESID_LN>(A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
+  return launch<QVIT_W8, EPI_RESID_LN>(A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
 }
 
 QVIT_GEMM_STAMP_READER  // diag_stamps.h: exists only in -DQVIT_GEMM_STAMPS builds

@@ -4,6 +4,7 @@
 // Every kernel reads its fp32 input once and writes int8 once (16 B per lane where the layout
 // allows), so the bound is HBM bandwidth: 5 bytes moved per element.
 #include "qvit_common.h"
+#include "ln_common.h"
 
 #include <algorithm>
 
@@ -284,17 +285,6 @@ __global__ __launch_bounds__(kThreads) void layernorm_quant_reg_kernel(
 
 // The same butterfly (xor 32, 16, 8, 4, 2, 1; identical sums in every lane) with the exact-xor steps on
 // permlane swaps and DPP instead of LDS shuffles.
-QVIT_DEV float wave_sum_fast(float v) {
-  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
-  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  v = __uint_as_float(b[0]) + __uint_as_float(b[1]);
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));  // row_ror:8
-  v += __shfl_xor(v, 4, 64);
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xf, 0xf, false));   // xor 2
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xf, 0xf, false));   // xor 1
-  return v;
-}
 
 // Persistent register-resident LayerNorm + quantizer (cols % 4 == 0, cols <= 256 * NV): each wave walks
 // rows wave, wave + nwaves, ... with the next row's load in flight while the current row is finished;
@@ -353,47 +343,18 @@ __global__ __launch_bounds__(kThreads, QVIT_LN_MINW) void layernorm_quant_persis
   for (; r < rows; r += nwaves) {
     float4 vn[NV];
     load_row(r + nwaves, vn);
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < NV; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
-    const float mean = wave_sum_fast(s) / (float)cols;
-    float s2 = 0.f;
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int64_t c = 4 * (lane + 64 * i);
-      if (c < cols) {
-        const float a = v[i].x - mean, b = v[i].y - mean, cc = v[i].z - mean, dd = v[i].w - mean;
-        s2 += (a * a + b * b) + (cc * cc + dd * dd);
-      }
-    }
-    const float var = wave_sum_fast(s2) / (float)cols;
-    const float rstd = 1.0f / sqrtf(var + eps);
+    uint32_t word[NV];
+    ln_quant_row<NV>(v, lane, (int)cols, eps,
+                     [&](int i, float4& gv, float4& bv) {
+                       gv = gbl[lane + 64 * i];
+                       bv = gbl[256 + lane + 64 * i];
+                     },
+                     ent, c0, inv_w, top, p, word);
     int8_t* cr = codes + r * ldc;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int64_t c = 4 * (lane + 64 * i);
-      if (c < cols) {
-        const float4 gv = gbl[lane + 64 * i], bv = gbl[256 + lane + 64 * i];
-        const float y[4] = {(v[i].x - mean) * rstd * gv.x + bv.x, (v[i].y - mean) * rstd * gv.y + bv.y,
-                            (v[i].z - mean) * rstd * gv.z + bv.z, (v[i].w - mean) * rstd * gv.w + bv.w};
-        uint32_t word;
-        if (ent != nullptr) {
-          uint2 e[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            e[j] = *epi_entry(ent, y[j], c0, inv_w, top);
-          epi_select_byte<0>(word, y[0], __uint_as_float(e[0].x), e[0].y);
-          epi_select_byte<1>(word, y[1], __uint_as_float(e[1].x), e[1].y);
-          epi_select_byte<2>(word, y[2], __uint_as_float(e[2].x), e[2].y);
-          epi_select_byte<3>(word, y[3], __uint_as_float(e[3].x), e[3].y);
-        } else {
-          word = (uint32_t)(uint8_t)to_i8_sat(quant_code(y[0], p)) |
-                 ((uint32_t)(uint8_t)to_i8_sat(quant_code(y[1], p)) << 8) |
-                 ((uint32_t)(uint8_t)to_i8_sat(quant_code(y[2], p)) << 16) |
-                 ((uint32_t)(uint8_t)to_i8_sat(quant_code(y[3], p)) << 24);
-        }
-        *reinterpret_cast<uint32_t*>(cr + c) = word;
-      }
+      if (c < cols) *reinterpret_cast<uint32_t*>(cr + c) = word[i];
     }
     for (int64_t c = cols + lane; c < kpad; c += 64) cr[c] = 0;
 #pragma unroll

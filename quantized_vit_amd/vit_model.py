@@ -21,6 +21,7 @@ from functools import partial
 from typing import Optional
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -28,6 +29,12 @@ import torch.nn.functional as F
 
 from . import _lib
 from .quant_layers import QuantizationMode, QuantizeConv2d, QuantizeLinear, epilogue_table, trace_codes
+
+# The residual GEMMs (proj, fc2) run the following LayerNorm + quantizer behind their tiles (qvit_gemm_resid_ln)
+# instead of as a separate launch when QVIT_FUSE_LN=1 (or FUSE_RESID_LN = True). Off by default: the fused
+# form is bit-identical but measured slower (the LayerNorm of a 128-row block
+# runs on the one workgroup that completes the block and stalls its tile pipeline).
+FUSE_RESID_LN = os.environ.get("QVIT_FUSE_LN", "0") == "1"
 
 # Benchmark instrumentation: when KERNEL_TIMING[name] is a list (name in "fc1", "fc2", "proj",
 # "qkv_attn", "ln"), the fused block appends a (start, end) HIP event pair recorded on the launch
@@ -237,17 +244,46 @@ class Block(nn.Module):
 
     def forward_fused_(self, x: torch.Tensor) -> torch.Tensor:
         """In-place fused block on a contiguous [B, N, C] fp32 residual buffer (owned by caller)."""
+        return self.forward_fused_chain_(x)[0]
+
+    def ln_fusable(self, x2: torch.Tensor, norm: nn.LayerNorm, p_res: QuantPlan) -> bool:
+        """Whether the residual GEMM with plan p_res can run `norm` (+ the next quantizer) behind its tiles."""
+        C = x2.shape[1]
+        return (FUSE_RESID_LN and p_res.n == C and C % 4 == 0 and C <= 1024 and x2.stride(0) == C
+                and x2.shape[0] * C * 4 < 2 ** 31 and norm.weight is not None and norm.bias is not None
+                and norm.weight.is_contiguous() and norm.bias.is_contiguous())
+
+    def resid_ln_(self, codes_in: torch.Tensor, p_res: QuantPlan, x2: torch.Tensor, norm: nn.LayerNorm,
+                  p_next: QuantPlan) -> torch.Tensor:
+        """x2 += layer(codes_in) (the proj / fc2 contraction), then norm(x2) quantized with p_next's activation
+        quantizer -> int8 codes [M, p_next.kpad] (qvit_gemm_resid_ln: one launch)."""
+        M, C = x2.shape
+        out = torch.empty((M, p_next.kpad), dtype=torch.int8, device=x2.device)
+        _lib.gemm_resid_ln(codes_in, M, p_res.kpad, p_res.packed, p_res.wfmt, p_res.n, p_res.npad, p_res.d_act,
+                           p_res.d_wt, p_res.bias_pad, x2, norm.weight, norm.bias, norm.eps, p_next.qtype,
+                           p_next.d_act, p_next.qm_act, p_next.t_act, 0, epilogue_table(p_next, _lib.EPI_I8), out,
+                           p_next.kpad)
+        return out
+
+    def forward_fused_chain_(self, x: torch.Tensor, codes_in: Optional[torch.Tensor] = None,
+                             next_block: Optional["Block"] = None):
+        """forward_fused_ with the LayerNorms carried by the residual GEMMs: `codes_in` = this block's norm1
+        codes when the previous block's fc2 produced them; with `next_block`, fc2 also produces that block's
+        norm1 codes. Returns (x, next_block's norm1 codes or None)."""
         B, N, C = x.shape
         M = B * N
         x2 = x.view(M, C)
         a, m = self.attn, self.mlp
         # x + attn(norm1(x))
         p_qkv = a.qkv.quant_plan()
-        codes = torch.empty((M, p_qkv.kpad), dtype=torch.int8, device=x.device)
-        with _timed("ln"):
-            _lib.layernorm_quant_i8(x2, self.norm1.weight, self.norm1.bias, self.norm1.eps, p_qkv.qtype,
-                                    p_qkv.d_act, p_qkv.qm_act, p_qkv.t_act, 0, codes, p_qkv.kpad,
-                                    code_table=epilogue_table(p_qkv, _lib.EPI_I8))
+        if codes_in is not None:
+            codes = codes_in
+        else:
+            codes = torch.empty((M, p_qkv.kpad), dtype=torch.int8, device=x.device)
+            with _timed("ln"):
+                _lib.layernorm_quant_i8(x2, self.norm1.weight, self.norm1.bias, self.norm1.eps, p_qkv.qtype,
+                                        p_qkv.d_act, p_qkv.qm_act, p_qkv.t_act, 0, codes, p_qkv.kpad,
+                                        code_table=epilogue_table(p_qkv, _lib.EPI_I8))
         trace_codes(a.qkv, codes, C)
         p_proj = a.proj.quant_plan()
         if (a.split_ok(p_qkv) and N <= _lib.QKV_ATT_MAX_N and p_qkv.wfmt == _lib.W4 and p_qkv.kpad <= 65536
@@ -262,9 +298,14 @@ class Block(nn.Module):
                                    p_qkv.bias_pad, a.num_heads, a.scale, out, _lib.ATT_I8, in_scale,
                                    p_proj.qtype, p_proj.d_act, p_proj.qm_act, p_proj.t_act, epi_table=tab)
             trace_codes(a.proj, out, p_proj.k)
+            p_fc1 = m.fc1.quant_plan()
+            if self.ln_fusable(x2, self.norm2, p_proj):
+                with _timed("proj"):
+                    ln_codes = self.resid_ln_(out, p_proj, x2, self.norm2, p_fc1)
+                return self._mlp_fused_(x, x2, M, ln_codes, next_block)
             with _timed("proj"):
                 a.proj.gemm_codes(out, p_proj, _lib.EPI_F32_RESID, out=x2)
-            return self._mlp_fused_(x, x2, M)
+            return self._mlp_fused_(x, x2, M, None, next_block)
         if a.split_ok(p_qkv):
             # qkv as pre-scaled fp16 hi/lo head planes, then attention + proj's activation quantizer
             in_scale = attention_in_scale(p_qkv)
@@ -280,7 +321,7 @@ class Block(nn.Module):
                                  epi_table=epilogue_table(p_proj, _lib.EPI_I8))
             trace_codes(a.proj, codes, p_proj.k)
             a.proj.gemm_codes(codes, p_proj, _lib.EPI_F32_RESID, out=x2)
-            return self._mlp_fused_(x, x2, M)
+            return self._mlp_fused_(x, x2, M, None, next_block)
         qkv = a.qkv.gemm_codes(codes, p_qkv, _lib.EPI_F32)
         if qkv.shape[1] != p_qkv.n:
             qkv = qkv[:, :p_qkv.n]
@@ -295,17 +336,22 @@ class Block(nn.Module):
             codes = a.proj._act_codes(h if h.is_contiguous() else h.contiguous(), p_proj)
         trace_codes(a.proj, codes, p_proj.k)
         a.proj.gemm_codes(codes, p_proj, _lib.EPI_F32_RESID, out=x2)
-        return self._mlp_fused_(x, x2, M)
+        return self._mlp_fused_(x, x2, M, None, next_block)
 
-    def _mlp_fused_(self, x: torch.Tensor, x2: torch.Tensor, M: int) -> torch.Tensor:
-        """x + mlp(norm2(x)) in place on the residual buffer."""
+    def _mlp_fused_(self, x: torch.Tensor, x2: torch.Tensor, M: int, codes_in: Optional[torch.Tensor] = None,
+                    next_block: Optional["Block"] = None):
+        """x + mlp(norm2(x)) in place on the residual buffer (codes_in: norm2's codes, from the proj GEMM).
+        Returns (x, next_block's norm1 codes when fc2 produced them, else None)."""
         m = self.mlp
         p_fc1 = m.fc1.quant_plan()
-        codes = torch.empty((M, p_fc1.kpad), dtype=torch.int8, device=x.device)
-        with _timed("ln"):
-            _lib.layernorm_quant_i8(x2, self.norm2.weight, self.norm2.bias, self.norm2.eps, p_fc1.qtype,
-                                    p_fc1.d_act, p_fc1.qm_act, p_fc1.t_act, 0, codes, p_fc1.kpad,
-                                    code_table=epilogue_table(p_fc1, _lib.EPI_I8))
+        if codes_in is not None:
+            codes = codes_in
+        else:
+            codes = torch.empty((M, p_fc1.kpad), dtype=torch.int8, device=x.device)
+            with _timed("ln"):
+                _lib.layernorm_quant_i8(x2, self.norm2.weight, self.norm2.bias, self.norm2.eps, p_fc1.qtype,
+                                        p_fc1.d_act, p_fc1.qm_act, p_fc1.t_act, 0, codes, p_fc1.kpad,
+                                        code_table=epilogue_table(p_fc1, _lib.EPI_I8))
         trace_codes(m.fc1, codes, p_fc1.k)
         p_fc2 = m.fc2.quant_plan()
         hid = torch.empty((M, p_fc2.kpad), dtype=torch.int8, device=x.device)
@@ -314,9 +360,13 @@ class Block(nn.Module):
         with _timed("fc1"):
             m.fc1.gemm_codes(codes, p_fc1, _lib.EPI_I8_GELU, out=hid, next_layer=m.fc2)
         trace_codes(m.fc2, hid, p_fc2.k)
+        if next_block is not None and self.ln_fusable(x2, next_block.norm1, p_fc2):
+            with _timed("fc2"):
+                nxt = self.resid_ln_(hid, p_fc2, x2, next_block.norm1, next_block.attn.qkv.quant_plan())
+            return x, nxt
         with _timed("fc2"):
             m.fc2.gemm_codes(hid, p_fc2, _lib.EPI_F32_RESID, out=x2)
-        return x
+        return x, None
 
     def forward(self, x):
         if self.fused_ok(x):
@@ -393,11 +443,17 @@ class VisionTransformer(nn.Module):
             else:
                 x = torch.cat((cls_token, self.dist_token.expand(x.shape[0], -1, -1), x), dim=1)
             x = self.pos_drop(x + self.pos_embed)
-        # the residual stream is a fresh buffer here, so fused blocks may update it in place
-        for blk in self.blocks:
+        # the residual stream is a fresh buffer here, so fused blocks may update it in place; a fused block's
+        # fc2 also runs the next fused block's norm1 (+ its qkv quantizer)
+        blocks = list(self.blocks)
+        codes = None
+        for i, blk in enumerate(blocks):
             if isinstance(blk, Block) and blk.fused_ok(x):
-                x = blk.forward_fused_(x.contiguous())
+                nb = blocks[i + 1] if i + 1 < len(blocks) else None
+                nb = nb if isinstance(nb, Block) and nb.fused_ok(x) else None
+                x, codes = blk.forward_fused_chain_(x.contiguous(), codes, nb)
             else:
+                codes = None
                 x = blk(x)
         # LayerNorm is per token: only the class (and distillation) token rows reach the heads
         if self.dist_token is None:

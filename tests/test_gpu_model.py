@@ -268,6 +268,24 @@ def test_vit_shipping_weight_codes_end_to_end(dev, qt):
     assert err <= 2.5 * floor + 1e-4, (err, floor)
 
 
+@pytest.mark.parametrize("name,depth,batch", [("vit_tiny_patch16_224", 4, 3), ("vit_base_patch16_224", 2, 5)])
+def test_vit_resid_ln_fusion_bit_identical(dev, name, depth, batch):
+    """The LayerNorms carried by the residual GEMMs (qvit_gemm_resid_ln: proj -> norm2, fc2 -> next norm1)
+    give the very same logits as the separate LayerNorm launches."""
+    model = build_quantized_vit(name, seed=6, depth=depth).to(dev)
+    img = synthetic_images(batch, 224, seed=2).to(dev)
+    outs = []
+    saved = vit_model.FUSE_RESID_LN
+    for fuse in (True, False):
+        vit_model.FUSE_RESID_LN = fuse
+        try:
+            with torch.no_grad():
+                outs.append(model(img).cpu())
+        finally:
+            vit_model.FUSE_RESID_LN = saved
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_vit_linear_quantizer_vs_oracle(dev):
     model = build_quantized_vit("vit_tiny_patch16_224", seed=5, quant_type=QuantizationType.SYMMETRIC_LINEAR).to(dev)
     cfg = O.ViTConfig(embed_dim=192, depth=12, num_heads=3, quant_type=O.LINEAR)

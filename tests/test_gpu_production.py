@@ -82,6 +82,63 @@ def test_gemm_b256_residual_epilogue(dev, N, K, layer):
     assert err < 1e-6, err
 
 
+def _resid_ln_case(dev, M, N, K, seed, qt=O.NONLINEAR, t=1.0, table=True):
+    """qvit_gemm_resid_ln against its two-launch form (qvit_gemm EPI_F32_RESID, then qvit_layernorm_quant_i8 on
+    the updated rows) on the same inputs: the residual rows and the LayerNorm codes must be bit-identical (the
+    LayerNorm behind the tiles runs the standalone kernel's row routine, ln_common.h)."""
+    from quantized_vit_amd.quant_layers import epilogue_table_geometry, saturation_level
+    a, w, A, packed, npad, kpad = _gemm_case(dev, M, N, K, seed=seed)
+    g = torch.Generator().manual_seed(seed + 1)
+    bias = torch.randn(N, generator=g) * 0.2
+    base = torch.randn(M, N, generator=g)
+    gamma = (torch.rand(N, generator=g) + 0.5).to(dev)
+    beta = (torch.randn(N, generator=g) * 0.1).to(dev)
+    d_a, d_w = 0.0123, 0.00457
+    qtc = _lib.QT_LINEAR if qt == O.LINEAR else _lib.QT_NONLINEAR
+    qmn, dn = 3.0, 3.0 ** t / 127
+    q = dict(out_d=_p(dn, dev), out_qm=_p(qmn, dev), out_t=_p(t, dev) if qt == O.NONLINEAR else None)
+    tab = None
+    if table:
+        geo = epilogue_table_geometry(qtc, dn, qmn, t, saturation_level(qtc, dn, qmn, t), False)
+        tab = _lib.epi_table_build(_lib.EPI_I8, qtc, q["out_d"], q["out_qm"], q["out_t"], 0, *geo, dev)
+    bias_pad = _lib.pad_bias(bias.to(dev), N, npad, dev)
+    kpad_c = (N + 127) // 128 * 128
+    # two-launch reference
+    x_ref = base.to(dev)
+    _lib.gemm(A, M, kpad, packed, _lib.W4, N, npad, _p(d_a, dev), _p(d_w, dev), bias_pad, _lib.EPI_F32_RESID, x_ref)
+    c_ref = torch.full((M, kpad_c), 77, dtype=torch.int8, device=dev)
+    _lib.layernorm_quant_i8(x_ref, gamma, beta, 1e-6, qtc, q["out_d"], q["out_qm"], q["out_t"], 0, c_ref, kpad_c,
+                            code_table=tab)
+    # fused, twice on the same arrival counters (they are never reset: each launch adds npad / 256 per row block)
+    for rep in range(2):
+        x = base.to(dev)
+        c = torch.full((M, kpad_c), 55, dtype=torch.int8, device=dev)
+        _lib.gemm_resid_ln(A, M, kpad, packed, _lib.W4, N, npad, _p(d_a, dev), _p(d_w, dev), bias_pad, x, gamma, beta,
+                           1e-6, qtc, q["out_d"], q["out_qm"], q["out_t"], 0, tab, c, kpad_c)
+        torch.cuda.synchronize()
+        assert torch.equal(x.cpu(), x_ref.cpu()), f"rep {rep}: residual rows differ"
+        dc = (c.cpu() != c_ref.cpu())
+        assert not dc.any(), f"rep {rep}: {int(dc.sum())} codes differ, first at {dc.nonzero()[0].tolist()}"
+    assert len(torch.unique(c_ref)) > 50
+    return c_ref
+
+
+@pytest.mark.parametrize("N,K,layer", [(768, 3072, "fc2"), (768, 768, "proj")])
+def test_gemm_resid_ln_b256(dev, N, K, layer):
+    """proj / fc2 with the next LayerNorm behind the tiles at the production size (1 182 tiles, 394 row
+    blocks, the LayerNorm of each by whichever of its 3 tile workgroups arrives last)."""
+    assert _tiles(M256, N) > 2 * BLOCKS_PER_CU * _cus(dev)
+    _resid_ln_case(dev, M256, N, K, seed=N + 5 * K)
+
+
+@pytest.mark.parametrize("M,N,K,qt,table", [(1000, 768, 768, O.LINEAR, True), (333, 192, 768, O.NONLINEAR, True),
+                                            (257, 1024, 1024, O.NONLINEAR, True), (300, 768, 768, O.NONLINEAR, False)])
+def test_gemm_resid_ln_shapes(dev, M, N, K, qt, table):
+    """Ragged row counts (a partial last row block), one tile per row block (N 192, ViT-Tiny), four (N 1024,
+    ViT-L), the linear quantizer, and the per-element quantizer without a code table."""
+    _resid_ln_case(dev, M, N, K, seed=M + N, qt=qt, table=table)
+
+
 @pytest.mark.parametrize("qt,t", [(O.NONLINEAR, 1.0), (O.LINEAR, 1.0)])
 def test_gemm_b256_gelu_code_epilogue(dev, qt, t):
     """fc1: d_a d_w acc + b -> GELU -> fc2's quantizer via the code table, int8 out (4 728 tiles)."""

@@ -30,6 +30,9 @@ SHAPES = {
     "fc1_i8nt": (M_B256, 3072, 768, _lib.EPI_I8),   # no code table: per-element quantizer
     "fc2": (M_B256, 768, 3072, _lib.EPI_F32_RESID),
     "big": (16384, 8192, 4096, _lib.EPI_I32),
+    # proj / fc2 with the next LayerNorm + quantizer behind the tiles (qvit_gemm_resid_ln)
+    "proj_ln": (M_B256, 768, 768, -1),
+    "fc2_ln": (M_B256, 768, 3072, -1),
 }
 
 
@@ -56,11 +59,24 @@ def run(name, M, N, K, epi, iters, dev, qtype=_lib.QT_NONLINEAR):
                                       epi == _lib.EPI_I8_GELU)
         if geo is not None:
             kw["epi_table"] = _lib.epi_table_build(epi, qtype, kw["out_d"], kw["out_qm"], kw["out_t"], 0, *geo, dev)
+    if epi == -1:
+        gamma, beta = torch.rand(N, device=dev) + 0.5, torch.randn(N, device=dev) * 0.1
+        codes = torch.empty((M, N), dtype=torch.int8, device=dev)
+        from quantized_vit_amd.quant_layers import epilogue_table_geometry, saturation_level
+        geo = epilogue_table_geometry(qtype, 4.0 / 127, 4.0, 1.0, saturation_level(qtype, 4.0 / 127, 4.0, 1.0), False)
+        tab = _lib.epi_table_build(_lib.EPI_I8, qtype, kw["out_d"], kw["out_qm"], kw["out_t"], 0, *geo, dev)
+
+    def launch():
+        if epi == -1:
+            _lib.gemm_resid_ln(A, M, K, packed, _lib.W4, N, npad, d_a, d_w, bias, C, gamma, beta, 1e-6, qtype,
+                               kw["out_d"], kw["out_qm"], kw["out_t"], 0, tab, codes, N)
+        else:
+            _lib.gemm(A, M, K, packed, _lib.W4, N, npad, d_a, d_w, bias, epi, C, **kw)
     times = []
     for i in range(iters + 3):
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
-        _lib.gemm(A, M, K, packed, _lib.W4, N, npad, d_a, d_w, bias, epi, C, **kw)
+        launch()
         e.record()
         times.append((s, e))
     torch.cuda.synchronize()

@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 DIAG = os.path.join(ROOT, "tools", "_diag")
 LIB = os.path.join(DIAG, "libqvit_hip_stamps.so")
-PHASES = ["head_wait", "dma_issue", "stage_wait", "reads+mfma", "epilogue", "tile_setup", "lgkm_wait"]
+PHASES = ["head_wait", "dma_issue", "stage_wait", "reads+mfma", "epilogue", "tile_setup", "ln_job"]
 
 
 def main():
