@@ -20,7 +20,7 @@ LIB = os.path.join(HERE, "libqvit_hip.so")
 ARCH = "gfx950"
 
 SOURCES = ["quant_kernels.hip", "gemm_w4a8.hip", "attention.hip", "qkv_attention.hip", "ultra_conv.hip"]
-HEADERS = ["qvit_common.h", "attn_common.h", "ln_common.h", "diag_stamps.h"]
+HEADERS = ["qvit_common.h", "attn_common.h", "attn32.h", "ln_common.h", "diag_stamps.h"]
 
 HIPCC_FLAGS = [
     f"--offload-arch={ARCH}",

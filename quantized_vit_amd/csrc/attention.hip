@@ -215,8 +215,19 @@ __global__ __launch_bounds__(256, 2) void attn_split_kernel(const _Float16* __re
   const int nqb = (N < QG ? (N + QB - 1) / QB : QG / QB);
   const int nkb = (N + KB - 1) / KB;
   const int per = nqb + nkb;
-  const int grid = gridDim.x;
-  const int my_units = (nunits - (int)blockIdx.x + grid - 1) / grid;
+  // units of this workgroup: with a grid that is a multiple of 8, XCD x (blocks x, x + 8, ...) owns a contiguous
+  // unit range, so the query groups of one (image, head) stream the same K / V through one XCD's L2 instead of
+  // fetching it once per XCD; otherwise units blockIdx + j * grid
+  const bool xcd_map = (gridDim.x & 7) == 0;
+  const int team = xcd_map ? (int)gridDim.x >> 3 : (int)gridDim.x;
+  const int slot = xcd_map ? (int)blockIdx.x >> 3 : (int)blockIdx.x;
+  int ulo = 0, uhi = nunits;
+  if (xcd_map) {
+    const int xcd = blockIdx.x & 7, per8 = nunits >> 3, rem = nunits & 7;
+    ulo = xcd * per8 + (xcd < rem ? xcd : rem);
+    uhi = ulo + per8 + (xcd < rem ? 1 : 0);
+  }
+  const int my_units = (uhi - ulo - slot + team - 1) / team;  // unit j: ulo + slot + j * team
   const int total = my_units * per;
   const int64_t plane = (int64_t)N * HD;
 
@@ -224,7 +235,7 @@ __global__ __launch_bounds__(256, 2) void attn_split_kernel(const _Float16* __re
   // DMA of stream block p into ring slot p % SRING
   auto issue = [&](int p) {
     const int j = p / per, idx = p - j * per;
-    const int unit = (int)blockIdx.x + j * grid;
+    const int unit = ulo + slot + j * team;
     const int grp = unit % ngroups, bh = unit / ngroups;
     const int h = bh % H, b = bh / H;
     const int64_t qoff = ((int64_t)b * 3 * H + h) * plane;
@@ -276,7 +287,7 @@ __global__ __launch_bounds__(256, 2) void attn_split_kernel(const _Float16* __re
   for (int p = 0; p < 3 && p < total; ++p) issue(p);
   int p = 0;
   for (int j = 0; j < my_units; ++j) {
-    const int unit = (int)blockIdx.x + j * grid;
+    const int unit = ulo + slot + j * team;
     const int grp = unit % ngroups, bh = unit / ngroups;
     const int h = bh % H, b = bh / H;
     const int q0 = grp * QG;

@@ -13,8 +13,10 @@
 //   ultra_wmax / ultra_wcodes : the weight quantizer (two passes: max|tanh|, then codes in the conv
 //                               kernel's K order (ky, kx, c)).
 //   ultra_bn_fold             : per-channel (alpha, beta) on the device.
-//   ultra_conv0               : layer 0 (float image input, 3 -> 16, 3x3): direct fp32 conv on the
-//                               VALU (27 taps), fused BN + quantizer + 2x2 max pool; NCHW in, NHWC codes out.
+//   ultra_conv0_mfma          : layer 0 (float image input, 3 -> 16, 3x3): implicit GEMM on
+//                               v_mfma_f32_16x16x32_f16 with fp16 hi/lo operand splits (fp32-class products),
+//                               fused BN + quantizer + 2x2 max pool; NCHW in, NHWC codes out.
+//   ultra_conv0_int_mfma      : the same layer of the integer deploy (uint8 image) on v_mfma_i32_16x16x64_i8.
 //   ultra_conv                : layers 1..8: implicit GEMM on v_mfma_i32_16x16x64_i8 over NHWC codes.
 //                               Block = 4 waves, 16x16 output pixels (each MFMA column tile is a 4x4
 //                               pixel patch, so a 2x2 pool window is lanes p, p^1, p^4, p^5), all output
@@ -74,62 +76,187 @@ QVIT_DEV int act_code(float x, float alpha, float shift, float levels) {
   return (int)rintf(fminf(fmaxf(y, 0.f), 1.f) * levels);
 }
 
-// ---- layer 0: float image, 3 -> 16 channels, 3x3 pad 1, BN + quantizer + 2x2 pool ----------------
-// One thread per pooled pixel (a 4x4x3 input window held in registers, 2x2 pre-pool pixels). The weights
-// (fake-quant values k/7, [16][3][3][3] as the reference lays them out) are read with wave-uniform
-// indices, so they arrive through scalar loads and feed the FMAs as SGPR operands; pixel pairs along x
-// run as packed fp32 FMAs. The output-channel loop is not unrolled, which keeps the register count low
-// enough for several waves per SIMD (the kernel waits on image loads, not on math).
-constexpr int C0_IN = 3, C0_OUT = 16, C0_K = C0_IN * 9;
-typedef float f2 __attribute__((ext_vector_type(2)));
+// ---- layer 0: 3 -> 16 channels, 3x3 pad 1, BN + quantizer + 2x2 pool -------------------------------
+constexpr int C0_OUT = 16;
 
-__global__ __launch_bounds__(256) void ultra_conv0_kernel(const float* __restrict__ img, int B, int H, int W,
-                                                          const float* __restrict__ wvals,
-                                                          const float* __restrict__ alpha,
-                                                          const float* __restrict__ shift, float levels,
-                                                          int8_t* __restrict__ out) {
+// ---- layer 0 on the matrix cores --------------------------------------------------------------------
+// The same conv as an implicit GEMM on v_mfma_f32_16x16x32_f16: A = 16 pixels (a 4x4 patch) x K taps, B = K x
+// the 16 output channels' weights, D[pixel][channel]. fp32 operands are exact sums of two fp16
+// (x = hi + lo, hi = RNE f16 of x, lo = RNE f16 of the exact x - hi: 22 significant bits) and the conv is
+// hi.hi + hi.lo + lo.hi with fp32 accumulation — the fp32 conv to ~2^-22 relative (the dropped lo.lo term),
+// the order of the 27-term sum aside. K order: 8-value groups g = lane >> 4 of two 4-channel pixel records (tap
+// (ky, kx); channel 3 a zero-weight pad). Chunk 0 = the 8 taps other than (2, 2): g < 3 = row g, kx 0 and 1;
+// g = 3 = kx 2, rows 0 and 1; its three passes are three MFMAs. Chunk 1 = tap (2, 2) with all three passes in one
+// MFMA: g = 0 is (x hi, x lo) against (w hi, w hi), g = 1 is (x hi, -) against (w lo, 0), g = 2, 3 zero weights.
+// 4 MFMAs per patch. (v_mfma_f32_16x16x16_f16 for a half-empty chunk gave wrong accumulator reads: the compiler
+// placed VALU reads of its result too early on gfx950.) The image tile is
+// staged once per tile as fp16 hi / lo planes of 4-channel pixels (8 B), so every pixel fragment is two 8-B LDS
+// reads and the hi / lo split runs once per input pixel instead of once per tap. The patch's row order puts
+// one 2x2 pool window in each lane's four D rows (row 4 G + j = window G, position j), so lane (window G,
+// channel n) pools in registers: BN is monotone in the accumulator (increasing for alpha >= 0, decreasing
+// below), so the pooled BN output is BN of the max (or min) accumulator, and the quantizer (monotone) runs
+// once per pooled value — the same code as pooling the four codes.
+// Tile staging: halo row hy = image row ty0 - 1 + hy, halo column hx = image column tx0 - 4 + hx (40 columns:
+// the conv reads hx = 3 .. 37), loaded as 4-pixel quads (one float4 / uchar4 per channel: 18 x 10 quads, one per
+// thread of the first 180) and written as four 4-channel pixel records.
+constexpr int C0_TY = 16, C0_TX = 32;                 // pre-pool output tile
+constexpr int C0_HY = C0_TY + 2, C0_HX = C0_TX + 8;   // halo rows, columns
+constexpr int C0_HPIX = C0_HY * C0_HX;
+constexpr int C0_PLANE = C0_HPIX * 8;                 // fp16 x 4 channels per pixel
+constexpr int C0_QUADS = C0_HY * C0_HX / 4;           // 180 <= 256
+static_assert(C0_QUADS <= 256, "one quad per thread");
+typedef _Float16 c0h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 c0h4 __attribute__((ext_vector_type(4)));
+typedef float c0f4 __attribute__((ext_vector_type(4)));
+
+QVIT_DEV float fmax_nn(float a, float b) { return __builtin_elementwise_maximum(a, b); }
+QVIT_DEV float fmin_nn(float a, float b) { return __builtin_elementwise_minimum(a, b); }
+QVIT_DEV _Float16 hi_h(float x) { return (_Float16)x; }
+// codes of lanes 4k .. 4k + 3 (channels n .. n + 3) as one word in lane 4k (DPP quad permutes)
+QVIT_DEV uint32_t pack_quad(int code) {
+  const uint32_t c1 = (uint32_t)__builtin_amdgcn_update_dpp(0, code, 0x39, 0xf, 0xf, false);  // quad lane + 1
+  const uint32_t c2 = (uint32_t)__builtin_amdgcn_update_dpp(0, code, 0x4E, 0xf, 0xf, false);  // + 2
+  const uint32_t c3 = (uint32_t)__builtin_amdgcn_update_dpp(0, code, 0x93, 0xf, 0xf, false);  // + 3
+  return ((uint32_t)code & 0xff) | ((c1 & 0xff) << 8) | ((c2 & 0xff) << 16) | (c3 << 24);
+}
+QVIT_DEV _Float16 lo_h(float x) { return (_Float16)(x - (float)(_Float16)x); }  // x - hi is exact in fp32
+
+template <bool VEC>
+__global__ __launch_bounds__(256, 4) void ultra_conv0_mfma_kernel(const float* __restrict__ img, int B, int H, int W,
+                                                               const float* __restrict__ wvals,
+                                                               const float* __restrict__ alpha,
+                                                               const float* __restrict__ shift, float levels,
+                                                               int8_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) int8_t smem[2][2 * C0_PLANE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n = lane & 15, g = lane >> 4;
+  // A row n = pixel (2 ((n >> 2) >> 1) + ((n & 3) >> 1), 2 ((n >> 2) & 1) + (n & 1)) of the 4x4 patch
+  const int py = 2 * (n >> 3) + ((n >> 1) & 1), px = 2 * ((n >> 2) & 1) + (n & 1);
   const int Ho = H / 2, Wo = W / 2;
-  const int64_t total = (int64_t)B * Ho * Wo;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int xo = (int)(i % Wo);
-    const int yo = (int)((i / Wo) % Ho);
-    const int b = (int)(i / ((int64_t)Wo * Ho));
-    float win[C0_IN][4][4];
+
+  // B operands: weights [o = n][c][ky][kx] split hi / lo in the K order above; record r (0, 1) of group g is tap
+  // (ky, kx) = g < 3 ? (g, r) : (r, 2)
+  c0h8 wh0, wl0, wc1;
 #pragma unroll
-    for (int c = 0; c < C0_IN; ++c)
+  for (int j = 0; j < 8; ++j) {
+    const int r = j >> 2, c = j & 3;
+    const int ky = g < 3 ? g : r, kx = g < 3 ? r : 2;
+    const float w = c < 3 ? wvals[((n * 3 + c) * 3 + ky) * 3 + kx] : 0.f;
+    wh0[j] = hi_h(w);
+    wl0[j] = lo_h(w);
+    const float w22 = c < 3 ? wvals[((n * 3 + c) * 3 + 2) * 3 + 2] : 0.f;
+    wc1[j] = g == 0 ? hi_h(w22) : (g == 1 && r == 0) ? lo_h(w22) : (_Float16)0;
+  }
+  const float al = alpha[n], sh = shift[n];
+  const bool up = !(al < 0.f);  // BN increasing in the accumulator
+
+  const int tiles_y = (H + C0_TY - 1) / C0_TY, tiles_x = (W + C0_TX - 1) / C0_TX;
+  const int ntiles = B * tiles_y * tiles_x;
+  const int64_t HW = (int64_t)H * W;
+  // this thread's halo quad (hy, 4 qx .. 4 qx + 3) of tile t -> registers (zero outside the image)
+  const int qy = tid / (C0_HX / 4), qx = tid - qy * (C0_HX / 4);
+  c0f4 xin[3];
+  auto load_tile = [&](int t) __attribute__((always_inline)) {
+    if (tid >= C0_QUADS) return;
+    const int tx0 = (t % tiles_x) * C0_TX, ty0 = ((t / tiles_x) % tiles_y) * C0_TY, b = t / (tiles_x * tiles_y);
+    const float* base = img + (int64_t)b * 3 * HW;
+    const int y = ty0 - 1 + qy, x = tx0 - 4 + 4 * qx;
+    const bool row = y >= 0 && y < H;
+    if (VEC) {  // W % 4 == 0: a quad is wholly inside or outside the row
+      const bool ok = row && x >= 0 && x < W;
+      const int64_t off = ok ? (int64_t)y * W + x : 0;
 #pragma unroll
-      for (int dy = 0; dy < 4; ++dy)
+      for (int c = 0; c < 3; ++c)
+        xin[c] = ok ? *reinterpret_cast<const c0f4*>(base + c * HW + off) : c0f4{0.f, 0.f, 0.f, 0.f};
+    } else {
 #pragma unroll
-        for (int dx = 0; dx < 4; ++dx) {
-          const int y = 2 * yo - 1 + dy, x = 2 * xo - 1 + dx;
-          win[c][dy][dx] = (y >= 0 && y < H && x >= 0 && x < W) ? img[(((int64_t)b * C0_IN + c) * H + y) * W + x] : 0.f;
+      for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool ok = row && x + e >= 0 && x + e < W;
+          xin[c][e] = ok ? base[c * HW + (int64_t)y * W + x + e] : 0.f;
         }
-    uint32_t words[4] = {0, 0, 0, 0};
-#pragma unroll 1
-    for (int o = 0; o < C0_OUT; ++o) {
-      const float* wo = wvals + o * C0_K;  // [c][ky][kx], wave-uniform
-      f2 acc0 = {0.f, 0.f}, acc1 = {0.f, 0.f};  // pre-pool rows 0 and 1, pixels (x, x+1)
-#pragma unroll
-      for (int c = 0; c < C0_IN; ++c)
-#pragma unroll
-        for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-          for (int kx = 0; kx < 3; ++kx) {
-            const float wv = wo[(c * 3 + ky) * 3 + kx];
-            const f2 w2 = {wv, wv};
-            acc0 = __builtin_elementwise_fma(f2{win[c][ky][kx], win[c][ky][kx + 1]}, w2, acc0);
-            acc1 = __builtin_elementwise_fma(f2{win[c][ky + 1][kx], win[c][ky + 1][kx + 1]}, w2, acc1);
-          }
-      const float al = alpha[o], sh = shift[o];
-      const int best = max(max(act_code(acc0.x, al, sh, levels), act_code(acc0.y, al, sh, levels)),
-                           max(act_code(acc1.x, al, sh, levels), act_code(acc1.y, al, sh, levels)));
-      const uint32_t v = (uint32_t)best << (8 * (o & 3));
-      if ((o >> 2) == 0) words[0] |= v;
-      else if ((o >> 2) == 1) words[1] |= v;
-      else if ((o >> 2) == 2) words[2] |= v;
-      else words[3] |= v;
     }
-    *reinterpret_cast<uint4*>(out + i * C0_OUT) = make_uint4(words[0], words[1], words[2], words[3]);
+  };
+  auto stage_tile = [&](int8_t* buf) __attribute__((always_inline)) {
+    if (tid >= C0_QUADS) return;
+    c0h8 hi[2], lo[2];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        hi[e >> 1][4 * (e & 1) + c] = hi_h(xin[c][e]);
+        lo[e >> 1][4 * (e & 1) + c] = lo_h(xin[c][e]);
+      }
+      hi[e >> 1][4 * (e & 1) + 3] = 0;
+      lo[e >> 1][4 * (e & 1) + 3] = 0;
+    }
+    int8_t* d = buf + 32 * tid;  // pixel (qy, 4 qx) = halo pixel 4 tid
+    *reinterpret_cast<c0h8*>(d) = hi[0];
+    *reinterpret_cast<c0h8*>(d + 16) = hi[1];
+    *reinterpret_cast<c0h8*>(d + C0_PLANE) = lo[0];
+    *reinterpret_cast<c0h8*>(d + C0_PLANE + 16) = lo[1];
+  };
+
+  int t = blockIdx.x;
+  if (t >= ntiles) return;
+  load_tile(t);
+  stage_tile(smem[0]);
+  __syncthreads();
+  for (int it = 0; t < ntiles; t += gridDim.x, ++it) {
+    const int8_t* buf = smem[it & 1];
+    const int tn = t + gridDim.x;
+    if (tn < ntiles) load_tile(tn);  // lands while this tile computes
+    const int tx0 = (t % tiles_x) * C0_TX, ty0 = ((t / tiles_x) % tiles_y) * C0_TY, b = t / (tiles_x * tiles_y);
+    const int yo = ((ty0 + 4 * wave) >> 1) + (g >> 1);  // this lane's pool window
+    // A fragment records (halo pixel of tap (ky, kx): row 4 wave + py + ky, column px + kx + 3, + 4 per patch):
+    // chunk 0 records r0, r1 of group g; chunk 1 = tap (2, 2) hi, then its lo (g = 0) or hi again
+    auto rec = [&](int ky, int kx) { return buf + ((4 * wave + py + ky) * C0_HX + px + kx + 3) * 8; };
+    const int8_t* r0 = g < 3 ? rec(g, 0) : rec(0, 2);
+    const int8_t* r1 = g < 3 ? rec(g, 1) : rec(1, 2);
+    const int8_t* c0 = rec(2, 2);
+    const int8_t* c1 = rec(2, 2) + (g == 0 ? C0_PLANE : 0);
+    // four patches at a time: their six-MFMA chains interleaved (a chain alone waits out each MFMA's latency)
+#pragma unroll
+    for (int pq = 0; pq < C0_TX / 4; pq += 4) {
+      c0h8 h0[4], l0[4], x1[4];
+      c0f4 acc[4];
+      auto pair = [](const int8_t* a, const int8_t* b) {
+        return __builtin_shufflevector(*reinterpret_cast<const c0h4*>(a), *reinterpret_cast<const c0h4*>(b), 0, 1, 2, 3,
+                                       4, 5, 6, 7);
+      };
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int o = 32 * (pq + q);
+        h0[q] = pair(r0 + o, r1 + o);
+        l0[q] = pair(r0 + C0_PLANE + o, r1 + C0_PLANE + o);
+        x1[q] = pair(c0 + o, c1 + o);
+        acc[q] = c0f4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(h0[q], wh0, acc[q], 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(x1[q], wc1, acc[q], 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(l0[q], wh0, acc[q], 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(h0[q], wl0, acc[q], 0, 0, 0);
+      // acc[q][j] = conv[pixel 4 g + j of patch pq + q][channel n]: window g's four pixels
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float mx = fmax_nn(fmax_nn(acc[q][0], acc[q][1]), fmax_nn(acc[q][2], acc[q][3]));
+        const float mn = fmin_nn(fmin_nn(acc[q][0], acc[q][1]), fmin_nn(acc[q][2], acc[q][3]));
+        const float y = __fadd_rn(__fmul_rn(up ? mx : mn, al), sh);
+        const int code = (int)rintf(__builtin_amdgcn_fmed3f(y, 0.f, 1.f) * levels);
+        const int xo = ((tx0 + 4 * (pq + q)) >> 1) + (g & 1);
+        const uint32_t word = pack_quad(code);
+        if ((n & 3) == 0 && yo < Ho && xo < Wo)
+          *reinterpret_cast<uint32_t*>(out + (((int64_t)b * Ho + yo) * Wo + xo) * C0_OUT + n) = word;
+      }
+    }
+    if (tn < ntiles) stage_tile(smem[(it + 1) & 1]);  // the other buffer: its last reader finished a barrier ago
+    __syncthreads();
   }
 }
 
@@ -145,56 +272,120 @@ QVIT_DEV int int_code(int acc, int inc, int bias, int sbits, int levels) {
   return (int)(v < 0 ? 0 : (v > levels ? levels : v));
 }
 
-// Layer 0 of the integer deploy: uint8 image NCHW (in_bit 8), weight codes [16][3][3][3] (reference layout),
-// int32 accumulation, integer threshold, 2x2 max pool on the codes -> NHWC codes [B][H/2][W/2][16].
-__global__ __launch_bounds__(256) void ultra_conv0_int_kernel(const uint8_t* __restrict__ img, int B, int H, int W,
-                                                              const int8_t* __restrict__ wcodes,
-                                                              const int* __restrict__ inc,
-                                                              const int* __restrict__ bias, int sbits, int levels,
-                                                              int8_t* __restrict__ out) {
+// Layer 0 of the integer deploy on v_mfma_i32_16x16x64_i8: the same tiling, pixel order and in-lane pool as
+// ultra_conv0_mfma_kernel, exact in int32. The uint8 image is staged as x - 128 (int8, 4-channel pixels), and
+// 128 * sum(w) per channel is added back to the accumulator; K = one 64-deep chunk, group g = kernel row g
+// (g < 3; group 3 zero weights), 16 values = kx 0..3 x c 0..3 (kx = 3, c = 3 zero-weight pads). The 2x2 pool
+// takes the max (inc >= 0) or min (inc < 0) accumulator before the threshold, which is monotone in acc * inc.
+constexpr int C0I_PLANE = C0_HPIX * 4;  // int8 x 4 channels per pixel
+
+template <bool VEC>
+__global__ __launch_bounds__(256, 4) void ultra_conv0_int_mfma_kernel(const uint8_t* __restrict__ img, int B, int H,
+                                                                   int W, const int8_t* __restrict__ wcodes,
+                                                                   const int* __restrict__ inc,
+                                                                   const int* __restrict__ bias, int sbits,
+                                                                   int levels, int8_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) int8_t smem[2][C0I_PLANE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n = lane & 15, g = lane >> 4;
+  const int py = 2 * (n >> 3) + ((n >> 1) & 1), px = 2 * ((n >> 2) & 1) + (n & 1);  // A row n (as the float kernel)
   const int Ho = H / 2, Wo = W / 2;
-  const int64_t total = (int64_t)B * Ho * Wo;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int xo = (int)(i % Wo);
-    const int yo = (int)((i / Wo) % Ho);
-    const int b = (int)(i / ((int64_t)Wo * Ho));
-    int win[C0_IN][4][4];
+
+  v4i wa;  // B operand: channel n, kernel row g, (kx, c) = (i >> 2, i & 3) for byte i
+  {
+    int8_t wb[16];
 #pragma unroll
-    for (int c = 0; c < C0_IN; ++c)
-#pragma unroll
-      for (int dy = 0; dy < 4; ++dy)
-#pragma unroll
-        for (int dx = 0; dx < 4; ++dx) {
-          const int y = 2 * yo - 1 + dy, x = 2 * xo - 1 + dx;
-          win[c][dy][dx] = (y >= 0 && y < H && x >= 0 && x < W) ? img[(((int64_t)b * C0_IN + c) * H + y) * W + x] : 0;
-        }
-    uint32_t words[4] = {0, 0, 0, 0};
-#pragma unroll 1
-    for (int o = 0; o < C0_OUT; ++o) {
-      const int8_t* wo = wcodes + o * C0_K;  // [c][ky][kx], wave-uniform
-      int a00 = 0, a01 = 0, a10 = 0, a11 = 0;
-#pragma unroll
-      for (int c = 0; c < C0_IN; ++c)
-#pragma unroll
-        for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-          for (int kx = 0; kx < 3; ++kx) {
-            const int wv = wo[(c * 3 + ky) * 3 + kx];
-            a00 += wv * win[c][ky][kx];
-            a01 += wv * win[c][ky][kx + 1];
-            a10 += wv * win[c][ky + 1][kx];
-            a11 += wv * win[c][ky + 1][kx + 1];
-          }
-      const int ic = inc[o], bc = bias[o];
-      const int best = max(max(int_code(a00, ic, bc, sbits, levels), int_code(a01, ic, bc, sbits, levels)),
-                           max(int_code(a10, ic, bc, sbits, levels), int_code(a11, ic, bc, sbits, levels)));
-      const uint32_t v = (uint32_t)best << (8 * (o & 3));
-      if ((o >> 2) == 0) words[0] |= v;
-      else if ((o >> 2) == 1) words[1] |= v;
-      else if ((o >> 2) == 2) words[2] |= v;
-      else words[3] |= v;
+    for (int i = 0; i < 16; ++i) {
+      const int kx = i >> 2, c = i & 3;
+      wb[i] = (g < 3 && kx < 3 && c < 3) ? wcodes[((n * 3 + c) * 3 + g) * 3 + kx] : (int8_t)0;
     }
-    *reinterpret_cast<uint4*>(out + i * C0_OUT) = make_uint4(words[0], words[1], words[2], words[3]);
+    wa = __builtin_bit_cast(v4i, wb);
+  }
+  // 128 sum(w) of channel n: the MFMA of an all-ones A with the weights
+  const v4i ones = v4i{0x01010101, 0x01010101, 0x01010101, 0x01010101};
+  const int wsum = 128 * __builtin_amdgcn_mfma_i32_16x16x64_i8(ones, wa, v4i{0, 0, 0, 0}, 0, 0, 0)[0];
+  const int ic = inc[n], bc = bias[n];
+
+  const int tiles_y = (H + C0_TY - 1) / C0_TY, tiles_x = (W + C0_TX - 1) / C0_TX;
+  const int ntiles = B * tiles_y * tiles_x;
+  const int64_t HW = (int64_t)H * W;
+  // this thread's halo quad (as the float kernel): per channel 4 bytes, staged as x - 128 in 4-channel pixels
+  const int qy = tid / (C0_HX / 4), qx = tid - qy * (C0_HX / 4);
+  uint32_t xin[3];
+  auto load_tile = [&](int t) __attribute__((always_inline)) {
+    if (tid >= C0_QUADS) return;
+    const int tx0 = (t % tiles_x) * C0_TX, ty0 = ((t / tiles_x) % tiles_y) * C0_TY, b = t / (tiles_x * tiles_y);
+    const uint8_t* base = img + (int64_t)b * 3 * HW;
+    const int y = ty0 - 1 + qy, x = tx0 - 4 + 4 * qx;
+    const bool row = y >= 0 && y < H;
+    if (VEC) {
+      const bool ok = row && x >= 0 && x < W;
+      const int64_t off = ok ? (int64_t)y * W + x : 0;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) xin[c] = ok ? *reinterpret_cast<const uint32_t*>(base + c * HW + off) : 0u;
+    } else {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool ok = row && x + e >= 0 && x + e < W;
+          w |= (uint32_t)(ok ? base[c * HW + (int64_t)y * W + x + e] : 0) << (8 * e);
+        }
+        xin[c] = w;
+      }
+    }
+  };
+  auto stage_tile = [&](int8_t* buf) __attribute__((always_inline)) {
+    if (tid >= C0_QUADS) return;
+    // pixel e of the quad: bytes (c0, c1, c2, 0) - 128 each (the pad byte becomes 0 again below)
+    v4i rec;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t p = ((xin[0] >> (8 * e)) & 0xff) | (((xin[1] >> (8 * e)) & 0xff) << 8) |
+                         (((xin[2] >> (8 * e)) & 0xff) << 16);
+      rec[e] = (int)((p ^ 0x00808080u));  // x - 128 as int8 == x ^ 0x80 for 0 <= x <= 255
+    }
+    *reinterpret_cast<v4i*>(buf + 16 * tid) = rec;
+  };
+
+  int t = blockIdx.x;
+  if (t >= ntiles) return;
+  load_tile(t);
+  stage_tile(smem[0]);
+  __syncthreads();
+  for (int it = 0; t < ntiles; t += gridDim.x, ++it) {
+    const int8_t* buf = smem[it & 1];
+    const int tn = t + gridDim.x;
+    if (tn < ntiles) load_tile(tn);
+    const int tx0 = (t % tiles_x) * C0_TX, ty0 = ((t / tiles_x) % tiles_y) * C0_TY, b = t / (tiles_x * tiles_y);
+    const int yo = ((ty0 + 4 * wave) >> 1) + (g >> 1);
+    // A fragment: pixels px .. px + 3 of kernel row g (group 3 re-reads row 2: zero weights)
+    const int8_t* bb = buf + ((4 * wave + py + (g < 3 ? g : 2)) * C0_HX + px + 3) * 4;
+#pragma unroll
+    for (int pq = 0; pq < C0_TX / 4; pq += 2) {
+      v4i acc[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(bb + 16 * (pq + q));
+        const v4i xb = v4i{(int)src[0], (int)src[1], (int)src[2], (int)src[3]};
+        acc[q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(xb, wa, v4i{0, 0, 0, 0}, 0, 0, 0);
+      }
+      // acc[q][j] + 128 sum(w) = conv[pixel 4 g + j of patch pq + q][channel n]
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int mx = max(max(acc[q][0], acc[q][1]), max(acc[q][2], acc[q][3]));
+        const int mn = min(min(acc[q][0], acc[q][1]), min(acc[q][2], acc[q][3]));
+        const int code = int_code((ic < 0 ? mn : mx) + wsum, ic, bc, sbits, levels);
+        const int xo = ((tx0 + 4 * (pq + q)) >> 1) + (g & 1);
+        const uint32_t word = pack_quad(code);
+        if ((n & 3) == 0 && yo < Ho && xo < Wo)
+          *reinterpret_cast<uint32_t*>(out + (((int64_t)b * Ho + yo) * Wo + xo) * C0_OUT + n) = word;
+      }
+    }
+    if (tn < ntiles) stage_tile(smem[(it + 1) & 1]);
+    __syncthreads();
   }
 }
 
@@ -368,6 +559,17 @@ __global__ void yolo_decode_kernel(const float* __restrict__ head, int B, int ny
   }
 }
 
+// persistent grid: every block resident at once (CUs x occupancy), at most one per tile
+template <class K>
+int64_t resident_grid(K kernel, int64_t ntiles) {
+  int dev = 0, cus = 0, occ = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                              hipSuccess || cus <= 0)
+    cus = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, 256, 0) != hipSuccess || occ <= 0) occ = 1;
+  return std::max<int64_t>(1, std::min<int64_t>(ntiles, (int64_t)cus * occ));
+}
+
 int grid_cap(int64_t work, int per = 256) {
   int64_t g = (work + per - 1) / per;
   if (g > 256 * 16) g = 256 * 16;
@@ -422,9 +624,19 @@ extern "C" int qvit_ultra_conv0(const float* img, int64_t B, int64_t H, int64_t 
   if ((((uintptr_t)out) & 15)) return QVIT_EALIGN;
   if (B * H * W > INT32_MAX) return QVIT_EINVAL;
   if (B == 0) return QVIT_OK;
-  const int64_t work = B * (H / 2) * (W / 2);
-  hipLaunchKernelGGL(ultra_conv0_kernel, dim3(grid_cap(work)), dim3(256), 0, stream, img, (int)B, (int)H, (int)W,
-                     wvals, alpha, shift, (float)((1 << a_bit) - 1), out);
+  // persistent over 16 x 32 tiles
+  const int64_t ntiles = B * ((H + C0_TY - 1) / C0_TY) * ((W + C0_TX - 1) / C0_TX);
+  if (ntiles > INT32_MAX) return QVIT_EINVAL;
+  const float levels = (float)((1 << a_bit) - 1);
+  if ((W % 4) == 0 && (((uintptr_t)img) & 15) == 0) {  // 16-B quad loads
+    const int64_t grid = resident_grid(ultra_conv0_mfma_kernel<true>, ntiles);
+    hipLaunchKernelGGL(ultra_conv0_mfma_kernel<true>, dim3((unsigned)grid), dim3(256), 0, stream, img, (int)B, (int)H,
+                       (int)W, wvals, alpha, shift, levels, out);
+  } else {
+    const int64_t grid = resident_grid(ultra_conv0_mfma_kernel<false>, ntiles);
+    hipLaunchKernelGGL(ultra_conv0_mfma_kernel<false>, dim3((unsigned)grid), dim3(256), 0, stream, img, (int)B, (int)H,
+                       (int)W, wvals, alpha, shift, levels, out);
+  }
   return qvit_hip_status(hipGetLastError());
 }
 
@@ -469,9 +681,17 @@ extern "C" int qvit_ultra_conv0_int(const uint8_t* img, int64_t B, int64_t H, in
   if ((((uintptr_t)out) & 15)) return QVIT_EALIGN;
   if (B * H * W > INT32_MAX) return QVIT_EINVAL;
   if (B == 0) return QVIT_OK;
-  const int64_t work = B * (H / 2) * (W / 2);
-  hipLaunchKernelGGL(ultra_conv0_int_kernel, dim3(grid_cap(work)), dim3(256), 0, stream, img, (int)B, (int)H, (int)W,
-                     wcodes, inc, bias, shift_bits, (1 << out_bit) - 1, out);
+  const int64_t ntiles = B * ((H + C0_TY - 1) / C0_TY) * ((W + C0_TX - 1) / C0_TX);
+  if (ntiles > INT32_MAX) return QVIT_EINVAL;
+  if ((W % 4) == 0 && (((uintptr_t)img) & 3) == 0) {  // 4-B quad loads
+    const int64_t grid = resident_grid(ultra_conv0_int_mfma_kernel<true>, ntiles);
+    hipLaunchKernelGGL(ultra_conv0_int_mfma_kernel<true>, dim3((unsigned)grid), dim3(256), 0, stream, img, (int)B,
+                       (int)H, (int)W, wcodes, inc, bias, shift_bits, (1 << out_bit) - 1, out);
+  } else {
+    const int64_t grid = resident_grid(ultra_conv0_int_mfma_kernel<false>, ntiles);
+    hipLaunchKernelGGL(ultra_conv0_int_mfma_kernel<false>, dim3((unsigned)grid), dim3(256), 0, stream, img, (int)B,
+                       (int)H, (int)W, wcodes, inc, bias, shift_bits, (1 << out_bit) - 1, out);
+  }
   return qvit_hip_status(hipGetLastError());
 }
 
