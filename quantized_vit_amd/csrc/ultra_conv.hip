@@ -420,7 +420,13 @@ __global__ __launch_bounds__(256, 2) void ultra_conv_kernel(const int8_t* __rest
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int p = lane & 15, g = lane >> 4;
-  const int py = p >> 2, px = p & 3;
+  // SW (pooled code layers): pixels are the MFMA A rows in the order of ultra_conv0_mfma_kernel (row 4 G + j =
+  // pool window G, position j), weights the B columns, so D[pixel][channel] puts each 2x2 window in one lane:
+  // the pool runs in registers on the accumulators (BN and the quantizer are monotone in them) and the
+  // quantizer once per pooled value. Otherwise A = weights, B = pixels (p = 4 py + px), D[channel][pixel].
+  constexpr bool SW = POOL != 0 && OUT != 1;
+  const int py = SW ? 2 * (p >> 3) + ((p >> 1) & 1) : p >> 2;
+  const int px = SW ? 2 * ((p >> 2) & 1) + (p & 1) : p & 3;
 
   // weights -> LDS once per block (rows >= real cout are zero in the packed image)
   for (int i = tid; i < COUT * (G::KPAD / 16); i += 256) {
@@ -440,6 +446,17 @@ __global__ __launch_bounds__(256, 2) void ultra_conv_kernel(const int8_t* __rest
       iinc[ct][j] = (OUT == 2 && o < cout_real) ? reinterpret_cast<const int*>(alpha)[o] : 0;
       ibias[ct][j] = (OUT == 2 && o < cout_real) ? reinterpret_cast<const int*>(shift)[o] : 0;
     }
+  // SW: this lane's channel 16 ct + p
+  float als[G::NCT], shs[G::NCT];
+  int iincs[G::NCT], ibiass[G::NCT];
+#pragma unroll
+  for (int ct = 0; ct < G::NCT; ++ct) {
+    const int o = 16 * ct + p;
+    als[ct] = (SW && OUT == 0 && o < cout_real) ? alpha[o] : 0.f;
+    shs[ct] = (SW && OUT == 0 && o < cout_real) ? shift[o] : 0.f;
+    iincs[ct] = (SW && OUT == 2 && o < cout_real) ? reinterpret_cast<const int*>(alpha)[o] : 0;
+    ibiass[ct] = (SW && OUT == 2 && o < cout_real) ? reinterpret_cast<const int*>(shift)[o] : 0;
+  }
 
   const int tiles_y = (H + TS - 1) / TS, tiles_x = (W + TS - 1) / TS;
   const int64_t ntiles = (int64_t)B * tiles_y * tiles_x;
@@ -483,7 +500,32 @@ __global__ __launch_bounds__(256, 2) void ultra_conv_kernel(const int8_t* __rest
       for (int pt = 0; pt < 4; ++pt)
 #pragma unroll
         for (int ct = 0; ct < G::NCT; ++ct)
-          acc[pt][ct] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[ct], bf[pt], acc[pt][ct], 0, 0, 0);
+          acc[pt][ct] = SW ? __builtin_amdgcn_mfma_i32_16x16x64_i8(bf[pt], a[ct], acc[pt][ct], 0, 0, 0)
+                           : __builtin_amdgcn_mfma_i32_16x16x64_i8(a[ct], bf[pt], acc[pt][ct], 0, 0, 0);
+    }
+
+    if constexpr (SW) {
+      // acc[pt][ct][j] = conv[b][cout 16 ct + p][pool window g of patch pt, position j]
+      const int Ho = H / 2, Wo = W / 2;
+      const int yo = ((ty0 + 4 * wave) >> 1) + (g >> 1);
+#pragma unroll
+      for (int pt = 0; pt < 4; ++pt) {
+        const int xo = ((tx0 + 4 * pt) >> 1) + (g & 1);
+#pragma unroll
+        for (int ct = 0; ct < G::NCT; ++ct) {
+          const v4i v = acc[pt][ct];
+          const int vmax = max(max(v[0], v[1]), max(v[2], v[3]));
+          const int vmin = min(min(v[0], v[1]), min(v[2], v[3]));
+          const int code = (OUT == 2) ? int_code(iincs[ct] < 0 ? vmin : vmax, iincs[ct], ibiass[ct], sbits, (int)levels)
+                                      : act_code((float)(als[ct] < 0.f ? vmin : vmax) / den, als[ct], shs[ct], levels);
+          const uint32_t word = pack_quad(code);  // channels 16 ct + p .. + 3 in lane p = 4k
+          const int o = 16 * ct + p;
+          if ((p & 3) == 0 && yo < Ho && xo < Wo && o < cout_real)
+            *reinterpret_cast<uint32_t*>(reinterpret_cast<int8_t*>(out) + (((int64_t)b * Ho + yo) * Wo + xo) * ldo + o) =
+                word;
+        }
+      }
+      continue;
     }
 
     // epilogue: acc[pt][ct][j] = conv[b][cout 16 ct + 4 g + j][y = ty0 + 4 wave + py][x = tx0 + 4 pt + px]
