@@ -574,16 +574,22 @@ __global__ __launch_bounds__(256, 2) void ultra_conv_kernel(const int8_t* __rest
 }
 
 // ---- YOLOLayer decode (mymodel.py:47-60) -----------------------------------------------------------
+// (32-bit index arithmetic: the launcher checks the element count fits; 64-bit divisions cost more than the
+// decode itself)
 __global__ void yolo_decode_kernel(const float* __restrict__ head, int B, int ny, int nx, int na, int no, int ldh,
                                    const float* __restrict__ anchors, float stride, float* __restrict__ io,
                                    float* __restrict__ pout) {
-  const int64_t total = (int64_t)B * na * ny * nx * no;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int o = (int)(i % no);
-    const int x = (int)((i / no) % nx);
-    const int y = (int)((i / ((int64_t)no * nx)) % ny);
-    const int a = (int)((i / ((int64_t)no * nx * ny)) % na);
-    const int b = (int)(i / ((int64_t)no * nx * ny * na));
+  const uint32_t total = (uint32_t)B * na * ny * nx * no;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    uint32_t r0 = i;
+    const int o = (int)(r0 % (uint32_t)no);
+    r0 /= (uint32_t)no;
+    const int x = (int)(r0 % (uint32_t)nx);
+    r0 /= (uint32_t)nx;
+    const int y = (int)(r0 % (uint32_t)ny);
+    r0 /= (uint32_t)ny;
+    const int a = (int)(r0 % (uint32_t)na);
+    const int b = (int)(r0 / (uint32_t)na);
     // p[b][a][y][x][o] = head_nchw[b][a*no + o][y][x] = head_nhwc[b][y][x][a*no + o]
     const float v = head[(((int64_t)b * ny + y) * nx + x) * ldh + a * no + o];
     pout[i] = v;
@@ -773,6 +779,7 @@ extern "C" int qvit_yolo_decode(const float* head, int64_t B, int64_t ny, int64_
                                 hipStream_t stream) {
   if (!head || !anchors || !io || !p) return QVIT_ENULL;
   if (B < 0 || ny < 1 || nx < 1 || na < 1 || no < 5 || ldh < na * no || !(stride > 0.f)) return QVIT_EINVAL;
+  if (B * na * ny * nx * no > (int64_t)INT32_MAX) return QVIT_EINVAL;  // the kernel's 32-bit element index
   if (B == 0) return QVIT_OK;
   hipLaunchKernelGGL(yolo_decode_kernel, dim3(grid_cap(B * na * ny * nx * no)), dim3(256), 0, stream, head, (int)B,
                      (int)ny, (int)nx, (int)na, (int)no, (int)ldh, anchors, stride, io, p);
