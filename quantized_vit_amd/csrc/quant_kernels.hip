@@ -154,33 +154,37 @@ __global__ __launch_bounds__(kThreads) void pad_bias_kernel(const float* __restr
 }
 
 // ---- conv input -> im2col codes ----------------------------------------------------------------
+// I: the index type of the element arithmetic (int when every extent fits: 64-bit divisions cost more than
+// the quantizer per 16-element chunk)
+template <typename I>
 __global__ __launch_bounds__(kThreads) void im2col_quant_kernel(
-    const float* __restrict__ x, int64_t B, int64_t C, int64_t H, int64_t W, int kh, int kw,
-    int sh, int sw, int ph, int pw, int dh, int dw, int64_t OH, int64_t OW, int qtype,
+    const float* __restrict__ x, int64_t B_, int64_t C_, int64_t H_, int64_t W_, int kh, int kw,
+    int sh, int sw, int ph, int pw, int dh, int dw, int64_t OH_, int64_t OW_, int qtype,
     const float* d, const float* qm, const float* t, int levels, int8_t* __restrict__ codes,
-    int64_t ldc, int64_t kpad) {
+    int64_t ldc_, int64_t kpad_) {
+  const I B = (I)B_, C = (I)C_, H = (I)H_, W = (I)W_, OH = (I)OH_, OW = (I)OW_, ldc = (I)ldc_, kpad = (I)kpad_;
   const QParams p = load_qparams(qtype, d, qm, t, levels);
-  const int64_t K = C * kh * kw;
-  const int64_t chunks_per_row = kpad / 16;
-  const int64_t rows = B * OH * OW;
-  const int64_t total = rows * chunks_per_row;
+  const I K = C * kh * kw;
+  const I chunks_per_row = kpad / 16;
+  const I rows = B * OH * OW;
+  const I total = rows * chunks_per_row;
   // patchify fast path: a 16-wide chunk is 16 consecutive pixels of one input row
   const bool patch16 = (kw % 16 == 0) && dw == 1 && pw == 0 && ph == 0 && (W % 4 == 0) &&
                        (sw % 4 == 0) && ((((uintptr_t)x) & 15) == 0);
-  for (int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; id < total;
-       id += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = id / chunks_per_row;
-    const int64_t c0 = (id - r * chunks_per_row) * 16;
-    const int64_t b = r / (OH * OW);
-    const int64_t rem = r - b * OH * OW;
-    const int64_t oh = rem / OW, ow = rem - (rem / OW) * OW;
+  for (I id = blockIdx.x * (I)blockDim.x + threadIdx.x; id < total;
+       id += (I)gridDim.x * blockDim.x) {
+    const I r = id / chunks_per_row;
+    const I c0 = (id - r * chunks_per_row) * 16;
+    const I b = r / (OH * OW);
+    const I rem = r - b * OH * OW;
+    const I oh = rem / OW, ow = rem - (rem / OW) * OW;
     float v[16];
     if (patch16 && c0 + 16 <= K) {
-      const int64_t ci = c0 / (kh * kw);
-      const int64_t r2 = c0 - ci * kh * kw;
-      const int64_t ih = r2 / kw, iw = r2 - ih * kw;
-      const int64_t y = oh * sh + ih * dh;
-      const int64_t xx = ow * sw + iw;
+      const I ci = c0 / (kh * kw);
+      const I r2 = c0 - ci * kh * kw;
+      const I ih = r2 / kw, iw = r2 - ih * kw;
+      const I y = oh * sh + ih * dh;
+      const I xx = ow * sw + iw;
       const float* src = x + ((b * C + ci) * H + y) * W + xx;
       if (y < H && xx + 16 <= W) {
 #pragma unroll
@@ -195,14 +199,14 @@ __global__ __launch_bounds__(kThreads) void im2col_quant_kernel(
     } else {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int64_t kk = c0 + i;
+        const I kk = c0 + i;
         float val = 0.f;
         if (kk < K) {
-          const int64_t ci = kk / (kh * kw);
-          const int64_t r2 = kk - ci * kh * kw;
-          const int64_t ih = r2 / kw, iw = r2 - ih * kw;
-          const int64_t y = oh * sh - ph + ih * dh;
-          const int64_t xx = ow * sw - pw + iw * dw;
+          const I ci = kk / (kh * kw);
+          const I r2 = kk - ci * kh * kw;
+          const I ih = r2 / kw, iw = r2 - ih * kw;
+          const I y = oh * sh - ph + ih * dh;
+          const I xx = ow * sw - pw + iw * dw;
           if (y >= 0 && y < H && xx >= 0 && xx < W) val = x[((b * C + ci) * H + y) * W + xx];
         }
         v[i] = val;
@@ -499,9 +503,15 @@ int qvit_im2col_quant_i8(const float* x, int64_t B, int64_t C, int64_t H, int64_
   if ((ldc % 16) || (((uintptr_t)codes) & 15)) return QVIT_EALIGN;
   if (B == 0) return QVIT_OK;
   const int64_t work = B * OH * OW * (kpad / 16);
-  hipLaunchKernelGGL(im2col_quant_kernel, dim3(grid_for(work, kThreads)), dim3(kThreads), 0, stream,
-                     x, B, C, H, W, kh, kw, sh, sw, ph, pw, dh, dw, OH, OW, qtype, d_quant, q_m,
-                     t_quant, levels, codes, ldc, kpad);
+  const int64_t lim = (int64_t)INT32_MAX - 2 * (int64_t)256 * 16 * kThreads;  // headroom for the grid stride
+  if (work < lim && B * C * H * W < lim && B * OH * OW * ldc < lim)
+    hipLaunchKernelGGL(im2col_quant_kernel<int>, dim3(grid_for(work, kThreads)), dim3(kThreads), 0, stream,
+                       x, B, C, H, W, kh, kw, sh, sw, ph, pw, dh, dw, OH, OW, qtype, d_quant, q_m,
+                       t_quant, levels, codes, ldc, kpad);
+  else
+    hipLaunchKernelGGL(im2col_quant_kernel<int64_t>, dim3(grid_for(work, kThreads)), dim3(kThreads), 0, stream,
+                       x, B, C, H, W, kh, kw, sh, sw, ph, pw, dh, dw, OH, OW, qtype, d_quant, q_m,
+                       t_quant, levels, codes, ldc, kpad);
   return qvit_hip_status(hipGetLastError());
 }
 
