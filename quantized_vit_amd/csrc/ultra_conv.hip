@@ -111,6 +111,24 @@ typedef float c0f4 __attribute__((ext_vector_type(4)));
 
 QVIT_DEV float fmax_nn(float a, float b) { return __builtin_elementwise_maximum(a, b); }
 QVIT_DEV float fmin_nn(float a, float b) { return __builtin_elementwise_minimum(a, b); }
+// Tiles of this persistent block: with a grid that is a multiple of 8, XCD x (blocks x, x + 8, ...) owns a
+// contiguous tile range, so the tiles in flight on one XCD are neighbours whose halo rows share 128-B lines
+// in that XCD's L2 (walking t = blockIdx + k grid put x-neighbours on different XCDs: layer 0 fetched 3.2x
+// its input from HBM). Tile k of this block: lo + slot + k team while < hi.
+struct TileWalk {
+  int lo, hi, slot, team;
+};
+QVIT_DEV TileWalk tile_walk(int ntiles) {
+  TileWalk w{0, ntiles, (int)blockIdx.x, (int)gridDim.x};
+  if ((gridDim.x & 7) == 0) {
+    const int xcd = blockIdx.x & 7, per = ntiles >> 3, rem = ntiles & 7;
+    w.lo = xcd * per + (xcd < rem ? xcd : rem);
+    w.hi = w.lo + per + (xcd < rem ? 1 : 0);
+    w.slot = blockIdx.x >> 3;
+    w.team = gridDim.x >> 3;
+  }
+  return w;
+}
 QVIT_DEV _Float16 hi_h(float x) { return (_Float16)x; }
 // codes of lanes 4k .. 4k + 3 (channels n .. n + 3) as one word in lane 4k (DPP quad permutes)
 QVIT_DEV uint32_t pack_quad(int code) {
@@ -199,15 +217,16 @@ __global__ __launch_bounds__(256, 4) void ultra_conv0_mfma_kernel(const float* _
     *reinterpret_cast<c0h8*>(d + C0_PLANE + 16) = lo[1];
   };
 
-  int t = blockIdx.x;
-  if (t >= ntiles) return;
+  const TileWalk tw = tile_walk(ntiles);
+  int t = tw.lo + tw.slot;
+  if (t >= tw.hi) return;
   load_tile(t);
   stage_tile(smem[0]);
   __syncthreads();
-  for (int it = 0; t < ntiles; t += gridDim.x, ++it) {
+  for (int it = 0; t < tw.hi; t += tw.team, ++it) {
     const int8_t* buf = smem[it & 1];
-    const int tn = t + gridDim.x;
-    if (tn < ntiles) load_tile(tn);  // lands while this tile computes
+    const int tn = t + tw.team;
+    if (tn < tw.hi) load_tile(tn);  // lands while this tile computes
     const int tx0 = (t % tiles_x) * C0_TX, ty0 = ((t / tiles_x) % tiles_y) * C0_TY, b = t / (tiles_x * tiles_y);
     const int yo = ((ty0 + 4 * wave) >> 1) + (g >> 1);  // this lane's pool window
     // A fragment records (halo pixel of tap (ky, kx): row 4 wave + py + ky, column px + kx + 3, + 4 per patch):
@@ -255,7 +274,7 @@ __global__ __launch_bounds__(256, 4) void ultra_conv0_mfma_kernel(const float* _
           *reinterpret_cast<uint32_t*>(out + (((int64_t)b * Ho + yo) * Wo + xo) * C0_OUT + n) = word;
       }
     }
-    if (tn < ntiles) stage_tile(smem[(it + 1) & 1]);  // the other buffer: its last reader finished a barrier ago
+    if (tn < tw.hi) stage_tile(smem[(it + 1) & 1]);  // the other buffer: its last reader finished a barrier ago
     __syncthreads();
   }
 }
@@ -350,15 +369,16 @@ __global__ __launch_bounds__(256, 4) void ultra_conv0_int_mfma_kernel(const uint
     *reinterpret_cast<v4i*>(buf + 16 * tid) = rec;
   };
 
-  int t = blockIdx.x;
-  if (t >= ntiles) return;
+  const TileWalk tw = tile_walk(ntiles);
+  int t = tw.lo + tw.slot;
+  if (t >= tw.hi) return;
   load_tile(t);
   stage_tile(smem[0]);
   __syncthreads();
-  for (int it = 0; t < ntiles; t += gridDim.x, ++it) {
+  for (int it = 0; t < tw.hi; t += tw.team, ++it) {
     const int8_t* buf = smem[it & 1];
-    const int tn = t + gridDim.x;
-    if (tn < ntiles) load_tile(tn);
+    const int tn = t + tw.team;
+    if (tn < tw.hi) load_tile(tn);
     const int tx0 = (t % tiles_x) * C0_TX, ty0 = ((t / tiles_x) % tiles_y) * C0_TY, b = t / (tiles_x * tiles_y);
     const int yo = ((ty0 + 4 * wave) >> 1) + (g >> 1);
     // A fragment: pixels px .. px + 3 of kernel row g (group 3 re-reads row 2: zero weights)
@@ -384,7 +404,7 @@ __global__ __launch_bounds__(256, 4) void ultra_conv0_int_mfma_kernel(const uint
           *reinterpret_cast<uint32_t*>(out + (((int64_t)b * Ho + yo) * Wo + xo) * C0_OUT + n) = word;
       }
     }
-    if (tn < ntiles) stage_tile(smem[(it + 1) & 1]);
+    if (tn < tw.hi) stage_tile(smem[(it + 1) & 1]);
     __syncthreads();
   }
 }
@@ -460,7 +480,8 @@ __global__ __launch_bounds__(256, 2) void ultra_conv_kernel(const int8_t* __rest
 
   const int tiles_y = (H + TS - 1) / TS, tiles_x = (W + TS - 1) / TS;
   const int64_t ntiles = (int64_t)B * tiles_y * tiles_x;
-  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+  const TileWalk tw = tile_walk((int)ntiles);
+  for (int64_t t = tw.lo + tw.slot; t < tw.hi; t += tw.team) {
     const int tx0 = (int)(t % tiles_x) * TS;
     const int ty0 = (int)((t / tiles_x) % tiles_y) * TS;
     const int b = (int)(t / ((int64_t)tiles_x * tiles_y));
