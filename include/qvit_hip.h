@@ -21,6 +21,9 @@
  *                             int8 x int4/int8 -> int32 MFMA contraction with a fused epilogue:
  *                             d_act * d_wt * acc + bias, optionally + residual (vit_model.py:206-207),
  *                             or GELU (vit_model.py:173) + the next layer's activation quantizer.
+ *   qvit_gemm_wonly           quant_layers.py:495-499 in the default WEIGHT_ONLY mode (quant_model.py:23): fp32
+ *                             activations x int4/int8 weight codes on bf16 MFMA (x split into three exact
+ *                             bf16 terms), d_wt * acc + bias — F.linear(x, quantize_weight(W), b).
  *   qvit_ultra_*              4-bit quantization/quant_ultra.py:8-91 + mymodel.py:62-144 (UltraNet: weight
  *                             codes, BN folding, fused conv+BN+quantizer+maxpool blocks, YOLO decode).
  *   qvit_attention            vit_model.py:133-149 (Attention.forward between qkv and proj):
@@ -178,6 +181,24 @@ int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda,
               int epilogue, void* C, int64_t ldc,
               int out_qtype, const float* out_d, const float* out_qm, const float* out_t,
               int out_levels, const void* epi_table, hipStream_t stream);
+
+/*
+ * Weight-only QuantizeLinear.forward (quant_layers.py:495-499, quant_mode WEIGHT_ONLY: quantize_act is the
+ * identity, :356-358): Y[m, n] = d_wt * sum_k X[m, k] k_w[n, k] + bias[n] with fp32 X.
+ *   X      : fp32 [M][ldx], K valid columns; K % QVIT_TILE_K == 0 (pad X with zero columns to the packed
+ *            kpad), ldx % 4 == 0, X 16-byte aligned.
+ *   Wp     : packed weights from qvit_pack_weight (wfmt, npad rows, kpad == K).
+ *   d_wt   : device float[1]; bias : device float[npad] (padded) or NULL.
+ *   Y      : fp32 [M][ldy], ldy % 4 == 0, 16-byte aligned; outputs for n >= N are not written.
+ *   workspace : optional device buffer (16-byte aligned, workspace_bytes long) for small M: with fewer tiles
+ *            than half the CUs the K range is split over several workgroups whose fp32 partials
+ *            (splits * M * npad floats) are then summed in a fixed order; NULL -> no split.
+ * fp32-GEMM accuracy: X is split into three bf16 terms whose sum is X exactly, every product with a code is
+ * exact in fp32, accumulation is fp32 (the order of the K-term sum differs from the reference's GEMM).
+ */
+int qvit_gemm_wonly(const float* X, int64_t M, int64_t K, int64_t ldx, const void* Wp, int wfmt,
+                    int64_t N, int64_t npad, const float* d_wt, const float* bias, float* Y, int64_t ldy,
+                    float* workspace, int64_t workspace_bytes, hipStream_t stream);
 
 /*
  * The residual contraction of a transformer block with the next LayerNorm behind it, in one launch:

@@ -62,6 +62,7 @@ _SIGNATURES = {
                                 _c_p, _i64, _i64, _c_p, _c_p],
     "qvit_gemm": [_c_p, _i64, _i64, _i64, _c_p, _i32, _i64, _i64, _c_p, _c_p, _c_p, _i32, _c_p, _i64,
                   _i32, _c_p, _c_p, _c_p, _i32, _c_p, _c_p],
+    "qvit_gemm_wonly": [_c_p, _i64, _i64, _i64, _c_p, _i32, _i64, _i64, _c_p, _c_p, _c_p, _i64, _c_p, _i64, _c_p],
     "qvit_epi_table_build": [_i32, _i32, _c_p, _c_p, _c_p, _i32, _f32, _f32, _i64, _c_p, _c_p],
     "qvit_gemm_resid_ln": [_c_p, _i64, _i64, _i64, _c_p, _i32, _i64, _i64, _c_p, _c_p, _c_p, _c_p, _i64, _c_p, _c_p,
                            _f32, _i32, _c_p, _c_p, _c_p, _i32, _c_p, _c_p, _i64, _i64, _c_p, _c_p],
@@ -227,6 +228,33 @@ def gemm(A: torch.Tensor, M: int, K: int, packed: torch.Tensor, wfmt: int, N: in
                             _ptr(bias_pad), epilogue, _ptr(C), C.stride(0), out_qtype, _ptr(out_d), _ptr(out_qm),
                             _ptr(out_t), out_levels, _ptr(epi_table), _stream(A.device)), "qvit_gemm")
     return C
+
+
+_WONLY_WS: dict = {}
+WONLY_WS_MAX = 64 << 20   # bytes of split-K partials kept per device (small-M weight-only layers)
+
+
+def wonly_workspace(device: torch.device, M: int, npad: int) -> Optional[torch.Tensor]:
+    """Split-K workspace of qvit_gemm_wonly for M rows (at most 256 partial sets), one buffer per device."""
+    need = min(256 * M * npad * 4, WONLY_WS_MAX)
+    buf = _WONLY_WS.get(str(device))
+    if buf is None or buf.numel() * 4 < need:
+        buf = torch.empty(need // 4 + 4, dtype=torch.float32, device=device)
+        _WONLY_WS[str(device)] = buf
+    return buf
+
+
+def gemm_wonly(X: torch.Tensor, M: int, K: int, packed: torch.Tensor, wfmt: int, N: int, npad: int,
+               d_wt: torch.Tensor, bias_pad: Optional[torch.Tensor], Y: torch.Tensor, split: bool = True) -> torch.Tensor:
+    """Y = d_wt * (X @ codes^T) + bias with fp32 X (qvit_gemm_wonly: weight-only QuantizeLinear); small M
+    splits the K range over several workgroups through a cached workspace (split=False: never)."""
+    _require_gpu(X, "activations")
+    small = (npad // 256) * ((M + 63) // 64) < 128   # the kernel splits K only for fewer tiles than this
+    ws = wonly_workspace(X.device, M, npad) if (split and small) else None
+    _check(load().qvit_gemm_wonly(_ptr(X), M, K, X.stride(0), _ptr(packed), wfmt, N, npad, _ptr(d_wt),
+                                  _ptr(bias_pad), _ptr(Y), Y.stride(0), _ptr(ws), 0 if ws is None else ws.numel() * 4,
+                                  _stream(X.device)), "qvit_gemm_wonly")
+    return Y
 
 
 _LN_COUNTERS: dict = {}

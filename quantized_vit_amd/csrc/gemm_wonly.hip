@@ -1,0 +1,293 @@
+// Weight-only QuantizeLinear.forward (quant_layers.py:495-499 with quant_mode = WEIGHT_ONLY, the reference's
+// default mode, quant_model.py:23): quantize_act is the identity (:356-358), so the layer is
+//   y = F.linear(x, quantize_weight(W), b) = x @ (d_w k)^T + b,   x fp32, k the int4 / int8 weight codes.
+// Here y = (d_w / s) * (x @ (s k)^T) + b on v_mfma_f32_16x16x32_bf16, with the codes read from the packed
+// image qvit_pack_weight writes for qvit_gemm (s = 16 for int4: the nibble in the high half of its byte).
+// Exactness: x = x1 + x2 + x3 with x1 = x truncated to bf16, x2 = (x - x1) truncated, x3 = x - x1 - x2 (each
+// difference is exact in fp32 and x3 has at most 8 significant bits, so x3 is a bf16 exactly); s k has at
+// most 7 significant bits, so every product x_i (s k) is exact in fp32 and the three passes sum x k with fp32
+// accumulation — an fp32 GEMM of x and k, the order of the K-term sum aside. One multiply by d_w / s (s a
+// power of two) and the bias add follow, as in the reference's fp32 F.linear on the fake-quant weight.
+//
+// Geometry: one workgroup (4 waves) per 64 (x rows) x 256 (weight rows) tile; wave w owns weight rows
+// [64 w, 64 w + 64) and all 64 x rows: 4 x 4 MFMA tiles of 16 x 16. K advances in 64-deep stages through
+// two LDS buffers: per stage each thread loads 16 fp32 of one x row (4 x 16 B) and its slice of the packed
+// weight stage (the GEMM's LDS image, 8 KiB int4 / 16 KiB int8) into registers while the current stage
+// computes, then splits the x values into three bf16 planes (rows padded to 144 B: conflict-free
+// ds_read_b128 fragment reads) and writes both to the other buffer; one barrier per stage.
+// MFMA operands: A = weights (16 rows), B = x (16 rows): lane (fr = l & 15, fq = l >> 4) pairs weight byte b of
+// its packed fragment with x column 16 fq + b of the stage (the qvit_gemm pairing), chunk c = bytes 8c .. 8c+7.
+// D[n][m]: acc[r][s][j] = y[m0 + 16 s + fr][n0 + 64 w + 16 fq + 4 r + j] (the packed rows are pre-permuted).
+// Few tiles (small M, e.g. one image): the K stages are split over `splits` workgroups per tile, each writing
+// its raw fp32 partial to a workspace, and wonly_reduce_kernel sums the partials in split order (deterministic)
+// and applies d_w / s and the bias.
+#include <algorithm>
+
+#include "qvit_common.h"
+
+namespace {
+
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+constexpr int WO_BM = 64;        // x rows per tile
+constexpr int WO_BN = 256;       // weight rows per tile (one packed tile_n)
+constexpr int WO_BK = 64;        // k per stage
+constexpr int WO_PITCH = 144;    // bytes per x-plane row: 64 bf16 + 16 pad
+constexpr int WO_PLANE = WO_BM * WO_PITCH;
+constexpr int WO_XBYTES = 3 * WO_PLANE;
+
+template <int WFMT>
+struct WoGeo {
+  static constexpr int WROW = WFMT == QVIT_W4 ? 32 : 64;  // packed bytes per weight row per stage
+  static constexpr int WBYTES = WO_BN * WROW;
+  static constexpr int WPER = WBYTES / 256 / 16;           // 16-B pieces per thread per stage
+  static constexpr int STAGE = WO_XBYTES + WBYTES;
+  static constexpr int MINB = WFMT == QVIT_W4 ? 2 : 1;
+};
+
+QVIT_DEV uint32_t nib16_lo(uint32_t p) { return (p << 4) & 0xF0F0F0F0u; }
+QVIT_DEV uint32_t nib16_hi(uint32_t p) { return p & 0xF0F0F0F0u; }
+QVIT_DEV uint32_t hi16(float a, float b) {  // bf16 bits of a (low half) and b (high half); both exact bf16 values
+  return (__float_as_uint(a) >> 16) | (__float_as_uint(b) & 0xFFFF0000u);
+}
+// four signed bytes -> four bf16 (exact: |byte| <= 128)
+QVIT_DEV void bytes_bf16(uint32_t d, uint32_t& lo, uint32_t& hi) {
+  const uint32_t u = d ^ 0x80808080u;  // unsigned byte = signed + 128
+  const float f0 = (float)(u & 0xff) - 128.f, f1 = (float)((u >> 8) & 0xff) - 128.f;
+  const float f2 = (float)((u >> 16) & 0xff) - 128.f, f3 = (float)(u >> 24) - 128.f;
+  lo = hi16(f0, f1);
+  hi = hi16(f2, f3);
+}
+QVIT_DEV float trunc_bf16(float x) { return __uint_as_float(__float_as_uint(x) & 0xFFFF0000u); }
+
+template <int WFMT>
+__global__ __launch_bounds__(256, WoGeo<WFMT>::MINB) void gemm_wonly_kernel(
+    const float* __restrict__ X, int M, int K, int64_t ldx, const int8_t* __restrict__ Wp, int N, int npad,
+    const float* __restrict__ d_wt, const float* __restrict__ bias, float* __restrict__ Y, int64_t ldy, int splits,
+    float* __restrict__ part) {
+  using G = WoGeo<WFMT>;
+  __shared__ __attribute__((aligned(16))) int8_t smem[2 * G::STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // tile: XCD x (blocks x, x + 8, ...) walks a contiguous range, weight tiles fastest, so the tiles of one
+  // x panel share an L2
+  const int nb_n = npad / WO_BN;
+  const int ntiles = nb_n * ((M + WO_BM - 1) / WO_BM);
+  int t, sp = 0;
+  if (splits > 1) {  // (tile, split) = (b / splits, b % splits)
+    t = (int)blockIdx.x / splits;
+    sp = (int)blockIdx.x - t * splits;
+  } else {
+    const int per = (ntiles + 7) >> 3;
+    t = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  }
+  if (t >= ntiles) return;
+  const int m0 = (t / nb_n) * WO_BM, tn = t % nb_n, n0 = tn * WO_BN;
+  const int nk = K / WO_BK;
+  const int ks0 = (int)((int64_t)sp * nk / splits), ks1 = (int)((int64_t)(sp + 1) * nk / splits);
+
+  // this thread's loads: x row m0 + (tid >> 2), columns 16 (tid & 3) .. + 15 of the stage; weight pieces
+  const int xr = tid >> 2, xq = tid & 3;
+  const int xm = (m0 + xr < M) ? m0 + xr : M - 1;  // rows past M: a valid row, never stored
+  const float* xsrc = X + (int64_t)xm * ldx + 16 * xq;
+  const int8_t* wsrc = Wp + (int64_t)tn * nk * G::WBYTES + tid * 16 * G::WPER;
+  f4 xv[4];
+  v4i wv[G::WPER];
+  auto load = [&](int kt) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xv[i] = *reinterpret_cast<const f4*>(xsrc + kt * WO_BK + 4 * i);
+#pragma unroll
+    for (int i = 0; i < G::WPER; ++i) wv[i] = *reinterpret_cast<const v4i*>(wsrc + (int64_t)kt * G::WBYTES + 16 * i);
+  };
+  // split and store into buffer b: plane p row xr, bf16 columns 16 xq .. + 15 (32 B)
+  auto store = [&](int b) __attribute__((always_inline)) {
+    int8_t* base = smem + b * G::STAGE;
+    uint32_t p1[8], p2[8], p3[8];
+#pragma unroll
+    for (int e = 0; e < 16; e += 2) {
+      const float a = xv[e >> 2][e & 3], c = xv[(e + 1) >> 2][(e + 1) & 3];
+      const float a1 = trunc_bf16(a), c1 = trunc_bf16(c);
+      const float ar = a - a1, cr = c - c1;  // exact
+      const float a2 = trunc_bf16(ar), c2 = trunc_bf16(cr);
+      const float a3 = ar - a2, c3 = cr - c2;  // exact, <= 8 significant bits
+      p1[e >> 1] = hi16(a1, c1);
+      p2[e >> 1] = hi16(a2, c2);
+      p3[e >> 1] = hi16(a3, c3);
+    }
+    int8_t* d = base + xr * WO_PITCH + 32 * xq;
+    *reinterpret_cast<uint4*>(d) = make_uint4(p1[0], p1[1], p1[2], p1[3]);
+    *reinterpret_cast<uint4*>(d + 16) = make_uint4(p1[4], p1[5], p1[6], p1[7]);
+    *reinterpret_cast<uint4*>(d + WO_PLANE) = make_uint4(p2[0], p2[1], p2[2], p2[3]);
+    *reinterpret_cast<uint4*>(d + WO_PLANE + 16) = make_uint4(p2[4], p2[5], p2[6], p2[7]);
+    *reinterpret_cast<uint4*>(d + 2 * WO_PLANE) = make_uint4(p3[0], p3[1], p3[2], p3[3]);
+    *reinterpret_cast<uint4*>(d + 2 * WO_PLANE + 16) = make_uint4(p3[4], p3[5], p3[6], p3[7]);
+#pragma unroll
+    for (int i = 0; i < G::WPER; ++i)
+      *reinterpret_cast<v4i*>(base + WO_XBYTES + tid * 16 * G::WPER + 16 * i) = wv[i];
+  };
+
+  // fragment offsets: weights as qvit_gemm's read_frags (XOR-swizzled packed image), x planes row 16 s + fr
+  const int woff = (WFMT == QVIT_W4) ? (64 * wave + fr) * G::WROW + ((fq ^ (((fr >> 3) & 1) << 1)) << 3)
+                                     : (64 * wave + fr) * G::WROW + ((fq ^ (((fr >> 2) & 1) << 1)) << 4);
+  const int xoff = fr * WO_PITCH + 32 * fq;
+
+  f4 acc[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc[r][s] = f4{0.f, 0.f, 0.f, 0.f};
+
+  load(ks0);
+  store(0);
+  __syncthreads();
+  for (int kt = ks0; kt < ks1; ++kt) {
+    const int cur = (kt - ks0) & 1;
+    if (kt + 1 < ks1) load(kt + 1);  // lands while this stage computes
+    const int8_t* base = smem + cur * G::STAGE;
+    // the wave's weight fragments of this stage as bf16: wb[r][c] = bytes 8c .. 8c + 7 of fragment r
+    bf8 wb[4][2];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v4i wf;
+      if (WFMT == QVIT_W4) {
+        const uint2 p = *reinterpret_cast<const uint2*>(base + WO_XBYTES + woff + r * 16 * G::WROW);
+        wf = v4i{(int)nib16_lo(p.x), (int)nib16_hi(p.x), (int)nib16_lo(p.y), (int)nib16_hi(p.y)};
+      } else {
+        wf = *reinterpret_cast<const v4i*>(base + WO_XBYTES + woff + r * 16 * G::WROW);
+      }
+      uint32_t h[8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bytes_bf16((uint32_t)wf[q], h[2 * q], h[2 * q + 1]);
+      wb[r][0] = __builtin_bit_cast(bf8, make_uint4(h[0], h[1], h[2], h[3]));
+      wb[r][1] = __builtin_bit_cast(bf8, make_uint4(h[4], h[5], h[6], h[7]));
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int8_t* xp = base + xoff + s * 16 * WO_PITCH + 16 * c;
+        const bf8 x1 = *reinterpret_cast<const bf8*>(xp);
+        const bf8 x2 = *reinterpret_cast<const bf8*>(xp + WO_PLANE);
+        const bf8 x3 = *reinterpret_cast<const bf8*>(xp + 2 * WO_PLANE);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r][s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[r][c], x1, acc[r][s], 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r][s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[r][c], x2, acc[r][s], 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r][s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[r][c], x3, acc[r][s], 0, 0, 0);
+      }
+    }
+    if (kt + 1 < ks1) store(cur ^ 1);  // the other buffer: its last reader finished a barrier ago
+    __syncthreads();
+  }
+
+  if (splits > 1) {  // raw partial -> part[sp][m][n] (n < npad, m < M)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int m = m0 + 16 * s + fr;
+      if (m >= M) continue;
+      float* pr = part + ((int64_t)sp * M + m) * npad + n0 + 64 * wave + 16 * fq;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) *reinterpret_cast<f4*>(pr + 4 * r) = acc[r][s];
+    }
+    return;
+  }
+  // epilogue: y = (d_w / s) acc + bias, 16 contiguous columns per lane and row (4 x 16-B stores)
+  const float alpha = (*d_wt) * (WFMT == QVIT_W4 ? 0.0625f : 1.f);
+  const int nb = n0 + 64 * wave + 16 * fq;
+  float bcol[16];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const f4 b4 = bias ? *reinterpret_cast<const f4*>(bias + nb + 4 * r) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bcol[4 * r + j] = b4[j];
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int m = m0 + 16 * s + fr;
+    if (m >= M) continue;
+    float* yr = Y + (int64_t)m * ldy + nb;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      f4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = fmaf(alpha, acc[r][s][j], bcol[4 * r + j]);
+      const int n = nb + 4 * r;
+      if (n + 4 <= N) {
+        *reinterpret_cast<f4*>(yr + 4 * r) = o;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (n + j < N) yr[4 * r + j] = o[j];
+      }
+    }
+  }
+}
+
+// y[m][n] = (d_w / s) sum_sp part[sp][m][n] + bias[n], the partials summed in split order
+template <int WFMT>
+__global__ __launch_bounds__(256) void wonly_reduce_kernel(const float* __restrict__ part, int splits, int M, int N,
+                                                            int npad, const float* __restrict__ d_wt,
+                                                            const float* __restrict__ bias, float* __restrict__ Y,
+                                                            int64_t ldy) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // one 4-column group per thread
+  const int gpr = npad / 4;
+  if (i >= (int64_t)M * gpr) return;
+  const int m = (int)(i / gpr), n = 4 * (int)(i - (int64_t)m * gpr);
+  if (n >= N) return;
+  f4 a = *reinterpret_cast<const f4*>(part + (int64_t)m * npad + n);
+  for (int sp = 1; sp < splits; ++sp) a += *reinterpret_cast<const f4*>(part + ((int64_t)sp * M + m) * npad + n);
+  const float alpha = (*d_wt) * (WFMT == QVIT_W4 ? 0.0625f : 1.f);
+  float* yr = Y + (int64_t)m * ldy + n;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (n + j < N) yr[j] = fmaf(alpha, a[j], bias ? bias[n + j] : 0.f);
+}
+
+}  // namespace
+
+extern "C" int qvit_gemm_wonly(const float* X, int64_t M, int64_t K, int64_t ldx, const void* Wp, int wfmt,
+                               int64_t N, int64_t npad, const float* d_wt, const float* bias, float* Y, int64_t ldy,
+                               float* workspace, int64_t workspace_bytes, hipStream_t stream) {
+  if (!X || !Wp || !Y || !d_wt) return QVIT_ENULL;
+  if (wfmt != QVIT_W4 && wfmt != QVIT_W8) return QVIT_EINVAL;
+  if (M < 0 || K <= 0 || K % QVIT_TILE_K || ldx < K || N <= 0 || npad < N || npad % WO_BN || ldy < N)
+    return QVIT_EINVAL;
+  if (M > INT32_MAX / 2 || npad > INT32_MAX / 2 || K > (1 << 24)) return QVIT_EINVAL;
+  if ((ldx % 4) || (((uintptr_t)X) & 15) || (((uintptr_t)Wp) & 15)) return QVIT_EALIGN;
+  if ((ldy % 4) || (((uintptr_t)Y) & 15) || (bias && (((uintptr_t)bias) & 15))) return QVIT_EALIGN;
+  if (M == 0) return QVIT_OK;
+  const int64_t ntiles = (npad / WO_BN) * ((M + WO_BM - 1) / WO_BM);
+  if (ntiles > INT32_MAX / 2) return QVIT_EINVAL;
+  // fewer tiles than half the CUs: split the K stages so that about 256 workgroups run (when the workspace
+  // holds the partials)
+  const int64_t nk = K / WO_BK;
+  int64_t splits = 1;
+  if (ntiles < 128 && nk >= 2 && workspace && !(((uintptr_t)workspace) & 15)) {
+    splits = std::min<int64_t>(nk, (256 + ntiles - 1) / ntiles);
+    while (splits > 1 && splits * M * npad * 4 > workspace_bytes) --splits;
+  }
+  const int64_t grid = splits > 1 ? ntiles * splits : (ntiles + 7) / 8 * 8;
+  const int8_t* w = reinterpret_cast<const int8_t*>(Wp);
+  if (wfmt == QVIT_W4)
+    hipLaunchKernelGGL(gemm_wonly_kernel<QVIT_W4>, dim3((unsigned)grid), dim3(256), 0, stream, X, (int)M, (int)K, ldx,
+                       w, (int)N, (int)npad, d_wt, bias, Y, ldy, (int)splits, workspace);
+  else
+    hipLaunchKernelGGL(gemm_wonly_kernel<QVIT_W8>, dim3((unsigned)grid), dim3(256), 0, stream, X, (int)M, (int)K, ldx,
+                       w, (int)N, (int)npad, d_wt, bias, Y, ldy, (int)splits, workspace);
+  if (splits > 1) {
+    const int64_t groups = M * (npad / 4);
+    const unsigned rg = (unsigned)((groups + 255) / 256);
+    if (wfmt == QVIT_W4)
+      hipLaunchKernelGGL(wonly_reduce_kernel<QVIT_W4>, dim3(rg), dim3(256), 0, stream, workspace, (int)splits, (int)M,
+                         (int)N, (int)npad, d_wt, bias, Y, ldy);
+    else
+      hipLaunchKernelGGL(wonly_reduce_kernel<QVIT_W8>, dim3(rg), dim3(256), 0, stream, workspace, (int)splits, (int)M,
+                         (int)N, (int)npad, d_wt, bias, Y, ldy);
+  }
+  return qvit_hip_status(hipGetLastError());
+}

@@ -322,15 +322,26 @@ class QuantizeMixin:
                 if int(overflow.item()) == 0:
                     plan.packed, plan.wfmt, plan.int_path = packed, wfmt, True
                     break
-        if plan.int_path:
+        if not wa and abs(lw) <= 127:
+            # weight-only mode (the reference's default): fp32 activations against the packed codes
+            # (qvit_gemm_wonly, QuantizeLinear); the same packing as the int path
+            overflow = torch.zeros(1, dtype=torch.int32, device=dev)
+            for wfmt in ((_lib.W4, _lib.W8) if abs(lw) <= 7 else (_lib.W8,)):
+                overflow.zero_()
+                packed = _lib.pack_weight(w32, qt_pack, d_pack, qm_pack, t_pack, wfmt, npad, kpad, overflow)
+                if int(overflow.item()) == 0:
+                    plan.packed, plan.wfmt = packed, wfmt
+                    plan.extra["wonly"] = True
+                    break
+        if plan.int_path or plan.extra.get("wonly"):
             bias = self.bias.detach() if self.bias is not None else None
             plan.bias_pad = _lib.pad_bias(bias, n, npad, dev)
             # |output| <= d_act d_wt sum_k |a_k||w_k| + |bias| <= d_act d_wt K L_a L_w + max|bias|
             plan.extra["out_bound"] = abs(s[3] * s[0]) * k * abs(la) * abs(lw) + s[-1]
         if wa:   # host copies of the activation quantizer's scalars (epilogue code tables of the producer)
             plan.extra["act_host"] = (qt, s[3], s[4], s[5] if t_act is not None else 1.0, la)
-        if not plan.int_path:   # weight-only mode, or levels that fit neither int4 nor int8 (e.g. 16/32 bits)
-            plan.w_fakequant = self._fake_quant_weight(plan)
+        if not plan.int_path and not plan.extra.get("wonly"):   # levels that fit neither int4 nor int8 (e.g. 16/32
+            plan.w_fakequant = self._fake_quant_weight(plan)     # bits); the fp32 form is otherwise filled lazily
         return plan
 
     def _fake_quant_weight(self, plan: QuantPlan) -> torch.Tensor:
@@ -522,9 +533,27 @@ class QuantizeLinear(nn.Linear, QuantizeMixin):
             if out.shape[1] != plan.n:
                 out = out[:, :plan.n].contiguous()
             return out.view(*input_.shape[:-1], plan.n)
+        if plan.extra.get("wonly"):
+            return self._forward_wonly(input_, plan)
         x = self.quantize_act(input_.float()) if self.quant_mode == QuantizationMode.WEIGHT_AND_ACTIVATION \
             else input_.float()
         return F.linear(x.detach(), self.w_fakequant(plan), None if self.bias is None else self.bias.detach())
+
+    def _forward_wonly(self, input_: torch.Tensor, plan: QuantPlan) -> torch.Tensor:
+        """Weight-only mode: F.linear(x, quantize_weight(W), b) as qvit_gemm_wonly on the packed codes."""
+        x2 = input_.detach().reshape(-1, plan.k)
+        M = x2.shape[0]
+        if (x2.dtype != torch.float32 or x2.stride(-1) != 1 or plan.k != plan.kpad or x2.stride(0) % 4
+                or x2.data_ptr() % 16):
+            xp = torch.zeros((M, plan.kpad), dtype=torch.float32, device=x2.device)
+            xp[:, :plan.k] = x2
+            x2 = xp
+        ldy = _round_up(plan.n, 4)
+        y = torch.empty((M, ldy), dtype=torch.float32, device=x2.device)
+        _lib.gemm_wonly(x2, M, plan.kpad, plan.packed, plan.wfmt, plan.n, plan.npad, plan.d_wt, plan.bias_pad, y)
+        if ldy != plan.n:
+            y = y[:, :plan.n].contiguous()
+        return y.view(*input_.shape[:-1], plan.n)
 
 
 class QuantizeConv2d(nn.Conv2d, QuantizeMixin):

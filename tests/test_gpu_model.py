@@ -113,14 +113,15 @@ def test_quantize_conv2d_int_path_vs_oracle(dev, cfg):
     assert rel(y, ref) < 1e-5
 
 
-def test_weight_only_mode_runs_fp_path(dev):
+def test_weight_only_mode_runs_wonly_kernel(dev):
+    """The default WEIGHT_ONLY mode: fp32 activations against the packed codes (qvit_gemm_wonly)."""
     torch.manual_seed(2)
     q = QuantizeLinear.from_module(nn.Linear(64, 32), quant_type=QuantizationType.SYMMETRIC_NONLINEAR,
                                    num_bits=4).to(dev).eval()
     x = torch.randn(5, 64)
     with torch.no_grad():
         y = q(x.to(dev))
-    assert not q.quant_plan().int_path
+    assert not q.quant_plan().int_path and q.quant_plan().extra.get("wonly")
     ref = O.quantize_linear(x, q.weight.detach().cpu(), q.bias.detach().cpu(), _layer_q(q))
     assert rel(y, ref) < 1e-5
 
