@@ -66,6 +66,10 @@ extern "C" {
 /* ---- GEMM weight storage ---------------------------------------------------------------- */
 #define QVIT_W4 4   /* int4 codes, 8 per uint32 (see qvit_pack_weight for the nibble order) */
 #define QVIT_W8 8   /* int8 codes                                                           */
+#define QVIT_W16 16 /* qvit_gemm_wonly only: codes |k| <= 32639 as balanced base-256 digits k = 256 h + l, h and l
+                       in [-128, 127], two QVIT_W8 images of npad * kpad bytes (h, then l; qvit_pack_weight)  */
+#define QVIT_W24 24 /* the same with three digits k = 65536 a + 256 h + l (|k| < 2^23, e.g. 16-bit layers whose
+                       saturation code is 32768): three QVIT_W8 images, a, h, l                               */
 
 /* ---- GEMM epilogues ----------------------------------------------------------------------- */
 #define QVIT_EPI_F32        0  /* C[m,n]  = d_act d_wt acc + bias[n]                 (fp32)          */
@@ -187,7 +191,8 @@ int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda,
  * identity, :356-358): Y[m, n] = d_wt * sum_k X[m, k] k_w[n, k] + bias[n] with fp32 X.
  *   X      : fp32 [M][ldx], K valid columns; K % QVIT_TILE_K == 0 (pad X with zero columns to the packed
  *            kpad), ldx % 4 == 0, X 16-byte aligned.
- *   Wp     : packed weights from qvit_pack_weight (wfmt, npad rows, kpad == K).
+ *   Wp     : packed weights from qvit_pack_weight (wfmt QVIT_W4 / QVIT_W8, npad rows, kpad == K), or QVIT_W16 /
+ *            QVIT_W24: the QVIT_W8 images of the balanced base-256 digits back to back (levels beyond int8).
  *   d_wt   : device float[1]; bias : device float[npad] (padded) or NULL.
  *   Y      : fp32 [M][ldy], ldy % 4 == 0, 16-byte aligned; outputs for n >= N are not written.
  *   workspace : optional device buffer (16-byte aligned, workspace_bytes long) for small M: with fewer tiles

@@ -25,6 +25,8 @@ QT_FORCE_CAREFUL = 0x100  # test-only: disable the guarded fast path
 
 W4 = 4
 W8 = 8
+W16 = 16  # qvit_gemm_wonly only: balanced base-256 digits as W8 images, two (|k| <= 32639) or
+W24 = 24  # three (|k| < 2^23)
 
 EPI_F32 = 0
 EPI_F32_RESID = 1
@@ -186,6 +188,33 @@ def pack_weight(w2d: torch.Tensor, qtype: int, d: torch.Tensor, qm: torch.Tensor
                                    _ptr(packed), npad, kpad, _ptr(overflow), _stream(w2d.device)),
            "qvit_pack_weight")
     return packed
+
+
+def pack_weight_wide(codes: torch.Tensor, npad: int, kpad: int):
+    """Packs integer weight codes beyond int8 ([n, k] float, on the device) for qvit_gemm_wonly as balanced
+    base-256 digits, one W8 image per digit, most significant first: W16 (k = 256 h + l, |k| <= 32639) or W24
+    (k = 65536 a + 256 h + l, |k| < 2^23). Returns (packed, wfmt)."""
+    _require_gpu(codes, "weight codes")
+    c = codes.detach().float().contiguous()
+    cmax = float(c.abs().max()) if c.numel() else 0.0
+    if cmax >= 2 ** 23:
+        raise QvitError("pack_weight_wide: a weight code reaches 2^23")
+    ndig = 2 if cmax <= 32639 else 3
+    digits = []
+    r = c
+    for _ in range(ndig):
+        d = torch.remainder(r + 128.0, 256.0) - 128.0   # in [-128, 127]
+        digits.append(d)
+        r = (r - d) / 256.0                              # exact: r - d is a multiple of 256
+    if float(r.abs().max()) if r.numel() else 0.0:
+        raise QvitError("pack_weight_wide: codes do not fit the digits")
+    one = torch.ones(1, device=c.device)
+    big = torch.full((1,), 1024.0, device=c.device)
+    ovf = torch.zeros(1, dtype=torch.int32, device=c.device)
+    imgs = [pack_weight(d.contiguous(), QT_LINEAR, one, big, None, W8, npad, kpad, ovf) for d in reversed(digits)]
+    if int(ovf.item()) != 0:
+        raise QvitError("pack_weight_wide: a digit left the int8 range")
+    return torch.cat(imgs), (W16 if ndig == 2 else W24)
 
 
 def pad_bias(bias: Optional[torch.Tensor], n: int, npad: int, device: torch.device) -> torch.Tensor:

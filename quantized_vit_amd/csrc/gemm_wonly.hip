@@ -18,6 +18,12 @@
 // MFMA operands: A = weights (16 rows), B = x (16 rows): lane (fr = l & 15, fq = l >> 4) pairs weight byte b of
 // its packed fragment with x column 16 fq + b of the stage (the qvit_gemm pairing), chunk c = bytes 8c .. 8c+7.
 // D[n][m]: acc[r][s][j] = y[m0 + 16 s + fr][n0 + 64 w + 16 fq + 4 r + j] (the packed rows are pre-permuted).
+// Wider codes (levels beyond int8, e.g. the reference's default num_bits = 16): balanced base-256 digits,
+// QVIT_W16 k = 256 h + l (|k| <= 32639), QVIT_W24 k = 65536 a + 256 h + l (|k| < 2^23; 16-bit layers whose
+// saturation code is 32768), every digit in [-128, 127], one QVIT_W8 image per digit, most significant first.
+// 65536 a, 256 h and l are bf16 exactly, every product with an x term is exact in fp32, the digits' terms stay
+// within about |k| (balanced: no cancellation beyond a factor 2), and one accumulator takes them all (three
+// MFMAs per x term and digit).
 // Few tiles (small M, e.g. one image): the K stages are split over `splits` workgroups per tile, each writing
 // its raw fp32 partial to a workspace, and wonly_reduce_kernel sums the partials in split order (deterministic)
 // and applies d_w / s and the bias.
@@ -40,10 +46,11 @@ constexpr int WO_XBYTES = 3 * WO_PLANE;
 
 template <int WFMT>
 struct WoGeo {
-  static constexpr int WROW = WFMT == QVIT_W4 ? 32 : 64;  // packed bytes per weight row per stage
-  static constexpr int WBYTES = WO_BN * WROW;
-  static constexpr int WPER = WBYTES / 256 / 16;           // 16-B pieces per thread per stage
-  static constexpr int STAGE = WO_XBYTES + WBYTES;
+  static constexpr int WROW = WFMT == QVIT_W4 ? 32 : 64;  // packed bytes per weight row per stage (per image)
+  static constexpr int PARTS = WFMT == QVIT_W24 ? 3 : WFMT == QVIT_W16 ? 2 : 1;  // digit images
+  static constexpr int WBYTES = WO_BN * WROW;              // one image's stage
+  static constexpr int WPER = PARTS * WBYTES / 256 / 16;   // 16-B pieces per thread per stage
+  static constexpr int STAGE = WO_XBYTES + PARTS * WBYTES;
   static constexpr int MINB = WFMT == QVIT_W4 ? 2 : 1;
 };
 
@@ -52,11 +59,11 @@ QVIT_DEV uint32_t nib16_hi(uint32_t p) { return p & 0xF0F0F0F0u; }
 QVIT_DEV uint32_t hi16(float a, float b) {  // bf16 bits of a (low half) and b (high half); both exact bf16 values
   return (__float_as_uint(a) >> 16) | (__float_as_uint(b) & 0xFFFF0000u);
 }
-// four signed bytes -> four bf16 (exact: |byte| <= 128)
-QVIT_DEV void bytes_bf16(uint32_t d, uint32_t& lo, uint32_t& hi) {
+// four signed bytes -> four bf16 of mul * byte, exact (mul a power of two)
+QVIT_DEV void bytes_bf16(uint32_t d, uint32_t& lo, uint32_t& hi, float mul) {
   const uint32_t u = d ^ 0x80808080u;  // unsigned byte = signed + 128
-  const float f0 = (float)(u & 0xff) - 128.f, f1 = (float)((u >> 8) & 0xff) - 128.f;
-  const float f2 = (float)((u >> 16) & 0xff) - 128.f, f3 = (float)(u >> 24) - 128.f;
+  const float f0 = ((float)(u & 0xff) - 128.f) * mul, f1 = ((float)((u >> 8) & 0xff) - 128.f) * mul;
+  const float f2 = ((float)((u >> 16) & 0xff) - 128.f) * mul, f3 = ((float)(u >> 24) - 128.f) * mul;
   lo = hi16(f0, f1);
   hi = hi16(f2, f3);
 }
@@ -94,14 +101,18 @@ __global__ __launch_bounds__(256, WoGeo<WFMT>::MINB) void gemm_wonly_kernel(
   const int xr = tid >> 2, xq = tid & 3;
   const int xm = (m0 + xr < M) ? m0 + xr : M - 1;  // rows past M: a valid row, never stored
   const float* xsrc = X + (int64_t)xm * ldx + 16 * xq;
-  const int8_t* wsrc = Wp + (int64_t)tn * nk * G::WBYTES + tid * 16 * G::WPER;
+  // (W16 / W24: piece i from digit image i / WPP, each image npad K bytes)
+  constexpr int WPP = G::WPER / G::PARTS;
+  const int8_t* wsrc = Wp + (int64_t)tn * nk * G::WBYTES + tid * 16 * WPP;
+  const int64_t wpart = (int64_t)npad * K;
   f4 xv[4];
   v4i wv[G::WPER];
   auto load = [&](int kt) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) xv[i] = *reinterpret_cast<const f4*>(xsrc + kt * WO_BK + 4 * i);
 #pragma unroll
-    for (int i = 0; i < G::WPER; ++i) wv[i] = *reinterpret_cast<const v4i*>(wsrc + (int64_t)kt * G::WBYTES + 16 * i);
+    for (int i = 0; i < G::WPER; ++i)
+      wv[i] = *reinterpret_cast<const v4i*>(wsrc + (i / WPP) * wpart + (int64_t)kt * G::WBYTES + 16 * (i % WPP));
   };
   // split and store into buffer b: plane p row xr, bf16 columns 16 xq .. + 15 (32 B)
   auto store = [&](int b) __attribute__((always_inline)) {
@@ -127,7 +138,7 @@ __global__ __launch_bounds__(256, WoGeo<WFMT>::MINB) void gemm_wonly_kernel(
     *reinterpret_cast<uint4*>(d + 2 * WO_PLANE + 16) = make_uint4(p3[4], p3[5], p3[6], p3[7]);
 #pragma unroll
     for (int i = 0; i < G::WPER; ++i)
-      *reinterpret_cast<v4i*>(base + WO_XBYTES + tid * 16 * G::WPER + 16 * i) = wv[i];
+      *reinterpret_cast<v4i*>(base + WO_XBYTES + (i / WPP) * G::WBYTES + tid * 16 * WPP + 16 * (i % WPP)) = wv[i];
   };
 
   // fragment offsets: weights as qvit_gemm's read_frags (XOR-swizzled packed image), x planes row 16 s + fr
@@ -148,37 +159,43 @@ __global__ __launch_bounds__(256, WoGeo<WFMT>::MINB) void gemm_wonly_kernel(
     const int cur = (kt - ks0) & 1;
     if (kt + 1 < ks1) load(kt + 1);  // lands while this stage computes
     const int8_t* base = smem + cur * G::STAGE;
-    // the wave's weight fragments of this stage as bf16: wb[r][c] = bytes 8c .. 8c + 7 of fragment r
-    bf8 wb[4][2];
+    // the wave's weight fragments of this stage as bf16: wb[q][r][c] = bytes 8c .. 8c + 7 of fragment r of
+    // digit image q, times 256^(PARTS - 1 - q)
+    bf8 wb[G::PARTS][4][2];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      v4i wf;
-      if (WFMT == QVIT_W4) {
-        const uint2 p = *reinterpret_cast<const uint2*>(base + WO_XBYTES + woff + r * 16 * G::WROW);
-        wf = v4i{(int)nib16_lo(p.x), (int)nib16_hi(p.x), (int)nib16_lo(p.y), (int)nib16_hi(p.y)};
-      } else {
-        wf = *reinterpret_cast<const v4i*>(base + WO_XBYTES + woff + r * 16 * G::WROW);
+    for (int q = 0; q < G::PARTS; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int8_t* wp = base + WO_XBYTES + q * G::WBYTES + woff + r * 16 * G::WROW;
+        v4i wf;
+        if (WFMT == QVIT_W4) {
+          const uint2 p = *reinterpret_cast<const uint2*>(wp);
+          wf = v4i{(int)nib16_lo(p.x), (int)nib16_hi(p.x), (int)nib16_lo(p.y), (int)nib16_hi(p.y)};
+        } else {
+          wf = *reinterpret_cast<const v4i*>(wp);
+        }
+        uint32_t h[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          bytes_bf16((uint32_t)wf[e], h[2 * e], h[2 * e + 1], G::PARTS - 1 - q == 2 ? 65536.f : G::PARTS - 1 - q == 1 ? 256.f : 1.f);
+        wb[q][r][0] = __builtin_bit_cast(bf8, make_uint4(h[0], h[1], h[2], h[3]));
+        wb[q][r][1] = __builtin_bit_cast(bf8, make_uint4(h[4], h[5], h[6], h[7]));
       }
-      uint32_t h[8];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) bytes_bf16((uint32_t)wf[q], h[2 * q], h[2 * q + 1]);
-      wb[r][0] = __builtin_bit_cast(bf8, make_uint4(h[0], h[1], h[2], h[3]));
-      wb[r][1] = __builtin_bit_cast(bf8, make_uint4(h[4], h[5], h[6], h[7]));
-    }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const int8_t* xp = base + xoff + s * 16 * WO_PITCH + 16 * c;
-        const bf8 x1 = *reinterpret_cast<const bf8*>(xp);
-        const bf8 x2 = *reinterpret_cast<const bf8*>(xp + WO_PLANE);
-        const bf8 x3 = *reinterpret_cast<const bf8*>(xp + 2 * WO_PLANE);
+        bf8 xs[3];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[r][s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[r][c], x1, acc[r][s], 0, 0, 0);
+        for (int p = 0; p < 3; ++p) xs[p] = *reinterpret_cast<const bf8*>(xp + p * WO_PLANE);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[r][s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[r][c], x2, acc[r][s], 0, 0, 0);
+        for (int q = 0; q < G::PARTS; ++q)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[r][s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[r][c], x3, acc[r][s], 0, 0, 0);
+          for (int p = 0; p < 3; ++p)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              acc[r][s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[q][r][c], xs[p], acc[r][s], 0, 0, 0);
       }
     }
     if (kt + 1 < ks1) store(cur ^ 1);  // the other buffer: its last reader finished a barrier ago
@@ -254,7 +271,7 @@ extern "C" int qvit_gemm_wonly(const float* X, int64_t M, int64_t K, int64_t ldx
                                int64_t N, int64_t npad, const float* d_wt, const float* bias, float* Y, int64_t ldy,
                                float* workspace, int64_t workspace_bytes, hipStream_t stream) {
   if (!X || !Wp || !Y || !d_wt) return QVIT_ENULL;
-  if (wfmt != QVIT_W4 && wfmt != QVIT_W8) return QVIT_EINVAL;
+  if (wfmt != QVIT_W4 && wfmt != QVIT_W8 && wfmt != QVIT_W16 && wfmt != QVIT_W24) return QVIT_EINVAL;
   if (M < 0 || K <= 0 || K % QVIT_TILE_K || ldx < K || N <= 0 || npad < N || npad % WO_BN || ldy < N)
     return QVIT_EINVAL;
   if (M > INT32_MAX / 2 || npad > INT32_MAX / 2 || K > (1 << 24)) return QVIT_EINVAL;
@@ -273,19 +290,21 @@ extern "C" int qvit_gemm_wonly(const float* X, int64_t M, int64_t K, int64_t ldx
   }
   const int64_t grid = splits > 1 ? ntiles * splits : (ntiles + 7) / 8 * 8;
   const int8_t* w = reinterpret_cast<const int8_t*>(Wp);
-  if (wfmt == QVIT_W4)
-    hipLaunchKernelGGL(gemm_wonly_kernel<QVIT_W4>, dim3((unsigned)grid), dim3(256), 0, stream, X, (int)M, (int)K, ldx,
-                       w, (int)N, (int)npad, d_wt, bias, Y, ldy, (int)splits, workspace);
-  else
-    hipLaunchKernelGGL(gemm_wonly_kernel<QVIT_W8>, dim3((unsigned)grid), dim3(256), 0, stream, X, (int)M, (int)K, ldx,
-                       w, (int)N, (int)npad, d_wt, bias, Y, ldy, (int)splits, workspace);
+#define QVIT_WO_LAUNCH(F)                                                                                    \
+  hipLaunchKernelGGL(gemm_wonly_kernel<F>, dim3((unsigned)grid), dim3(256), 0, stream, X, (int)M, (int)K, ldx, w, \
+                     (int)N, (int)npad, d_wt, bias, Y, ldy, (int)splits, workspace)
+  if (wfmt == QVIT_W4) QVIT_WO_LAUNCH(QVIT_W4);
+  else if (wfmt == QVIT_W8) QVIT_WO_LAUNCH(QVIT_W8);
+  else if (wfmt == QVIT_W16) QVIT_WO_LAUNCH(QVIT_W16);
+  else QVIT_WO_LAUNCH(QVIT_W24);
+#undef QVIT_WO_LAUNCH
   if (splits > 1) {
     const int64_t groups = M * (npad / 4);
     const unsigned rg = (unsigned)((groups + 255) / 256);
     if (wfmt == QVIT_W4)
       hipLaunchKernelGGL(wonly_reduce_kernel<QVIT_W4>, dim3(rg), dim3(256), 0, stream, workspace, (int)splits, (int)M,
                          (int)N, (int)npad, d_wt, bias, Y, ldy);
-    else
+    else  // (W8 / W16 / W24 accumulators are unscaled)
       hipLaunchKernelGGL(wonly_reduce_kernel<QVIT_W8>, dim3(rg), dim3(256), 0, stream, workspace, (int)splits, (int)M,
                          (int)N, (int)npad, d_wt, bias, Y, ldy);
   }

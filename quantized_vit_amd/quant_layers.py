@@ -322,17 +322,25 @@ class QuantizeMixin:
                 if int(overflow.item()) == 0:
                     plan.packed, plan.wfmt, plan.int_path = packed, wfmt, True
                     break
-        if not wa and abs(lw) <= 127:
-            # weight-only mode (the reference's default): fp32 activations against the packed codes
-            # (qvit_gemm_wonly, QuantizeLinear); the same packing as the int path
-            overflow = torch.zeros(1, dtype=torch.int32, device=dev)
-            for wfmt in ((_lib.W4, _lib.W8) if abs(lw) <= 7 else (_lib.W8,)):
-                overflow.zero_()
-                packed = _lib.pack_weight(w32, qt_pack, d_pack, qm_pack, t_pack, wfmt, npad, kpad, overflow)
-                if int(overflow.item()) == 0:
-                    plan.packed, plan.wfmt = packed, wfmt
-                    plan.extra["wonly"] = True
-                    break
+        if not plan.int_path and abs(lw) <= 65536:
+            # fp32 activations against the packed weight codes (qvit_gemm_wonly, QuantizeLinear): the weight-only
+            # mode (the reference's default) and W+A layers off the int path (levels beyond int8: their
+            # activations are fake-quantized to fp32 first); int4 / int8 codes as on the int path, wider ones
+            # (e.g. the default num_bits = 16) as balanced base-256 digits (W16 / W24)
+            if abs(lw) <= 127:
+                overflow = torch.zeros(1, dtype=torch.int32, device=dev)
+                for wfmt in ((_lib.W4, _lib.W8) if abs(lw) <= 7 else (_lib.W8,)):
+                    overflow.zero_()
+                    packed = _lib.pack_weight(w32, qt_pack, d_pack, qm_pack, t_pack, wfmt, npad, kpad, overflow)
+                    if int(overflow.item()) == 0:
+                        plan.packed, plan.wfmt = packed, wfmt
+                        plan.extra["wonly"] = True
+                        break
+            else:
+                wc = codes.to(device=dev, dtype=torch.float32) if codes is not None else \
+                    (_lib.fake_quant_f32(w32, qt, d_wt, qm_wt, t_wt) / d_wt).round()
+                plan.packed, plan.wfmt = _lib.pack_weight_wide(wc, npad, kpad)
+                plan.extra["wonly"] = True
         if plan.int_path or plan.extra.get("wonly"):
             bias = self.bias.detach() if self.bias is not None else None
             plan.bias_pad = _lib.pad_bias(bias, n, npad, dev)
@@ -534,7 +542,9 @@ class QuantizeLinear(nn.Linear, QuantizeMixin):
                 out = out[:, :plan.n].contiguous()
             return out.view(*input_.shape[:-1], plan.n)
         if plan.extra.get("wonly"):
-            return self._forward_wonly(input_, plan)
+            x = self.quantize_act(input_.float()) if self.quant_mode == QuantizationMode.WEIGHT_AND_ACTIVATION \
+                else input_
+            return self._forward_wonly(x, plan)
         x = self.quantize_act(input_.float()) if self.quant_mode == QuantizationMode.WEIGHT_AND_ACTIVATION \
             else input_.float()
         return F.linear(x.detach(), self.w_fakequant(plan), None if self.bias is None else self.bias.detach())

@@ -142,6 +142,9 @@ def test_weight_and_activation_wide_bits_fp_path(dev, bits, qt):
     with torch.no_grad():
         y, yc = lin(x.to(dev)), conv(img.to(dev))
     assert not lin.quant_plan().int_path and not conv.quant_plan().int_path
+    # 16 bits: the linear layer runs qvit_gemm_wonly on wide codes (fake-quant fp32 activations); 32 bits: F.linear
+    assert bool(lin.quant_plan().extra.get("wonly")) == (bits == 16)
+    assert bits != 16 or lin.quant_plan().wfmt in (_lib.W16, _lib.W24)
     ref = O.quantize_linear(x, lin.weight.detach().cpu(), lin.bias.detach().cpu(), _layer_q(lin))
     refc = O.quantize_conv2d(img, conv.weight.detach().cpu(), conv.bias.detach().cpu(), _layer_q(conv), stride=4,
                              padding=0)

@@ -101,6 +101,52 @@ def test_gemm_wonly_split_k(dev, wfmt, M, N, K):
         _check_close(y, x, codes, 0.02, bias)
 
 
+@pytest.mark.parametrize("lim", [32639, 32768, 5000000])
+@pytest.mark.parametrize("M,N,K", [(1, 40, 96), (77, 300, 768), (197, 768, 3072), (700, 512, 256)])
+def test_gemm_wonly_wide_vs_fp64(dev, M, N, K, lim):
+    """Codes beyond int8 as balanced base-256 digits: W16 (|k| <= 32639) and W24 (the 16-bit saturation code
+    32768 and wider), including the extreme codes and the digit boundaries."""
+    g = torch.Generator().manual_seed(M + N + K + lim)
+    codes = torch.randint(-lim, lim + 1, (N, K), generator=g).float()
+    codes.view(-1)[:8] = torch.tensor([lim, -lim, 127., 128., -128., -129., 255., -1.])
+    codes = codes.to(dev)
+    x = torch.randn(M, K, generator=g).to(dev)
+    bias = torch.randn(N, generator=g).to(dev)
+    npad, kpad = (N + 255) // 256 * 256, (K + 127) // 128 * 128
+    packed, wfmt = _lib.pack_weight_wide(codes, npad, kpad)
+    assert wfmt == (_lib.W16 if lim <= 32639 else _lib.W24)
+    xp = torch.zeros((M, kpad), device=dev)
+    xp[:, :K] = x
+    for split in (True, False):
+        y = torch.full((M, (N + 3) // 4 * 4), float("nan"), device=dev)
+        _lib.gemm_wonly(xp, M, kpad, packed, wfmt, N, npad, _p(3e-5, dev), _lib.pad_bias(bias, N, npad, dev), y,
+                        split=split)
+        torch.cuda.synchronize()
+        _check_close(y[:, :N], x, codes, 3e-5, bias)
+
+
+@pytest.mark.parametrize("mode", [QuantizationMode.WEIGHT_ONLY, QuantizationMode.WEIGHT_AND_ACTIVATION])
+@pytest.mark.parametrize("qt", [QuantizationType.SYMMETRIC_NONLINEAR, QuantizationType.SYMMETRIC_LINEAR])
+def test_default_16bit_linear_vs_oracle(dev, qt, mode):
+    """model_to_quantize_model's defaults (num_bits = 16, quant_model.py:21-23): 32767 levels per side run
+    qvit_gemm_wonly on W16 codes (W+A: the activations fake-quantized to fp32 first) and match the oracle's fp32
+    fake-quant F.linear."""
+    torch.manual_seed(16)
+    q = QuantizeLinear.from_module(nn.Linear(768, 200), quant_type=qt, quant_mode=mode, num_bits=16).to(dev).eval()
+    plan = q.quant_plan()
+    assert plan.extra.get("wonly") and plan.wfmt in (_lib.W16, _lib.W24) and not plan.int_path
+    x = torch.randn(2, 30, 768)
+    with torch.no_grad():
+        y = q(x.to(dev))
+    sd = {k: v.detach().cpu() for k, v in q.state_dict().items()}
+    lq = O.LayerQ.from_state(sd, "", q.quant_type.value, q.quant_mode.value)
+    ref = O.quantize_linear(x, sd["weight"], sd["bias"], lq)
+    xq = O.qact(x, lq) if mode == QuantizationMode.WEIGHT_AND_ACTIVATION else x
+    mag = xq.reshape(-1, 768).abs().double() @ O.qweight(sd["weight"], lq).abs().double().t() + sd["bias"].abs().double()
+    err = (y.cpu().reshape(-1, 200).double() - ref.reshape(-1, 200).double()).abs()
+    assert (err <= 2 * TOL * mag).all(), float((err / mag).max())
+
+
 def test_gemm_wonly_production_size(dev):
     """The ViT-B/16 b256 fc1 shape (M = 50 432) in weight-only mode: many tiles per XCD range, the fp64
     reference on the device."""
