@@ -376,6 +376,20 @@ class QuantizeMixin:
         _lib.quantize_act_i8(w, plan.qtype, plan.d_wt, plan.qm_wt, plan.t_wt, 0, codes, plan.kpad)
         return codes[:, :w.shape[1]].float()
 
+    def _wonly_rows(self, x2: torch.Tensor, plan: QuantPlan) -> torch.Tensor:
+        """[M, k] fp32 rows (or rows already zero-padded to kpad columns) @ quantize_weight(W)^T + b on
+        qvit_gemm_wonly (weight-only / wide-level plans)."""
+        M = x2.shape[0]
+        if (x2.dtype != torch.float32 or x2.stride(-1) != 1 or x2.shape[1] < plan.kpad or x2.stride(0) % 4
+                or x2.data_ptr() % 16):
+            xp = torch.zeros((M, plan.kpad), dtype=torch.float32, device=x2.device)
+            xp[:, :plan.k] = x2[:, :plan.k]
+            x2 = xp
+        ldy = _round_up(plan.n, 4)
+        y = torch.empty((M, ldy), dtype=torch.float32, device=x2.device)
+        _lib.gemm_wonly(x2, M, plan.kpad, plan.packed, plan.wfmt, plan.n, plan.npad, plan.d_wt, plan.bias_pad, y)
+        return y if ldy == plan.n else y[:, :plan.n]
+
     def w_fakequant(self, plan: QuantPlan) -> torch.Tensor:
         """The reference's quantize_weight(W) (quant_layers.py:332-354), cached on the plan."""
         if plan.w_fakequant is None:
@@ -544,26 +558,11 @@ class QuantizeLinear(nn.Linear, QuantizeMixin):
         if plan.extra.get("wonly"):
             x = self.quantize_act(input_.float()) if self.quant_mode == QuantizationMode.WEIGHT_AND_ACTIVATION \
                 else input_
-            return self._forward_wonly(x, plan)
+            y = self._wonly_rows(x.detach().reshape(-1, plan.k), plan)
+            return y.reshape(*input_.shape[:-1], plan.n)
         x = self.quantize_act(input_.float()) if self.quant_mode == QuantizationMode.WEIGHT_AND_ACTIVATION \
             else input_.float()
         return F.linear(x.detach(), self.w_fakequant(plan), None if self.bias is None else self.bias.detach())
-
-    def _forward_wonly(self, input_: torch.Tensor, plan: QuantPlan) -> torch.Tensor:
-        """Weight-only mode: F.linear(x, quantize_weight(W), b) as qvit_gemm_wonly on the packed codes."""
-        x2 = input_.detach().reshape(-1, plan.k)
-        M = x2.shape[0]
-        if (x2.dtype != torch.float32 or x2.stride(-1) != 1 or plan.k != plan.kpad or x2.stride(0) % 4
-                or x2.data_ptr() % 16):
-            xp = torch.zeros((M, plan.kpad), dtype=torch.float32, device=x2.device)
-            xp[:, :plan.k] = x2
-            x2 = xp
-        ldy = _round_up(plan.n, 4)
-        y = torch.empty((M, ldy), dtype=torch.float32, device=x2.device)
-        _lib.gemm_wonly(x2, M, plan.kpad, plan.packed, plan.wfmt, plan.n, plan.npad, plan.d_wt, plan.bias_pad, y)
-        if ldy != plan.n:
-            y = y[:, :plan.n].contiguous()
-        return y.view(*input_.shape[:-1], plan.n)
 
 
 class QuantizeConv2d(nn.Conv2d, QuantizeMixin):
@@ -625,6 +624,18 @@ class QuantizeConv2d(nn.Conv2d, QuantizeMixin):
             return out[:, :n].reshape(B, OH, OW, n).permute(0, 3, 1, 2).contiguous()
         x = self.quantize_act(input_.float()) if self.quant_mode == QuantizationMode.WEIGHT_AND_ACTIVATION \
             else input_.float()
+        if plan.extra.get("wonly") and self._int_conv_ok():
+            # weight-only / wide levels: the input patches (K order (c, kh, kw) = the weight flattening) as fp32
+            # rows against the packed codes (qvit_gemm_wonly)
+            B = x.shape[0]
+            cols = F.unfold(x.detach(), self.kernel_size, self.dilation, self.padding, self.stride)  # [B, K, L]
+            L = cols.shape[2]
+            OH = (x.shape[2] + 2 * self.padding[0] - self.dilation[0] * (self.kernel_size[0] - 1) - 1) // self.stride[0] + 1
+            OW = L // OH
+            x2 = torch.zeros((B * L, plan.kpad), dtype=torch.float32, device=x.device)
+            x2.view(B, L, plan.kpad)[:, :, :plan.k] = cols.transpose(1, 2)
+            y = self._wonly_rows(x2, plan)
+            return y.reshape(B, OH, OW, plan.n).permute(0, 3, 1, 2).contiguous()
         w = self.w_fakequant(plan).view_as(self.weight)
         return F.conv2d(x.detach(), w, None if self.bias is None else self.bias.detach(), self.stride,
                         self.padding, self.dilation, self.groups)

@@ -221,3 +221,29 @@ def test_weight_only_bound_codes(dev):
     assert q.quant_plan().extra.get("wonly")
     d_w = float(q.d_quant_wt.detach().reshape(-1)[0])
     _check_close(y, x, codes.to(dev), d_w, q.bias.detach())
+
+
+@pytest.mark.parametrize("bits", [4, 16])
+@pytest.mark.parametrize("cfg", [dict(cin=3, cout=768, k=16, s=16, p=0, H=224), dict(cin=16, cout=40, k=3, s=2, p=1, H=15)])
+def test_weight_only_conv2d_vs_oracle(dev, cfg, bits):
+    """QuantizeConv2d in WEIGHT_ONLY mode (the patch embedding and a padded strided conv): the input patches as
+    fp32 rows against the packed codes on qvit_gemm_wonly, vs the oracle's fp32 F.conv2d on the fake-quant weight
+    (quant_layers.py:575-587)."""
+    import torch.nn.functional as F
+    from quantized_vit_amd.quant_layers import QuantizeConv2d
+    torch.manual_seed(bits + cfg["k"])
+    conv = nn.Conv2d(cfg["cin"], cfg["cout"], cfg["k"], stride=cfg["s"], padding=cfg["p"], bias=True)
+    q = QuantizeConv2d.from_module(conv, quant_type=QuantizationType.SYMMETRIC_NONLINEAR,
+                                   quant_mode=QuantizationMode.WEIGHT_ONLY, num_bits=bits).to(dev).eval()
+    assert q.quant_plan().extra.get("wonly")
+    x = torch.randn(2, cfg["cin"], cfg["H"], cfg["H"])
+    with torch.no_grad():
+        y = q(x.to(dev))
+    sd = {k: v.detach().cpu() for k, v in q.state_dict().items()}
+    lq = O.LayerQ.from_state(sd, "", q.quant_type.value, q.quant_mode.value)
+    ref = O.quantize_conv2d(x, sd["weight"], sd["bias"], lq, stride=cfg["s"], padding=cfg["p"])
+    assert y.shape == ref.shape and y.is_contiguous()
+    mag = F.conv2d(x.abs().double(), O.qweight(sd["weight"], lq).abs().double(), sd["bias"].abs().double(),
+                   stride=cfg["s"], padding=cfg["p"])
+    err = (y.cpu().double() - ref.double()).abs()
+    assert (err <= 2 * TOL * mag).all(), float((err / mag).max())
