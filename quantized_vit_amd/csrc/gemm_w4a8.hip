@@ -6,9 +6,9 @@
 //   block tile 256 (n, weights) x 128 (m, activations); k advances in 64-deep stages.
 //   Wave w owns weight rows [64w, 64w+64) and all 128 activation rows: 4 x 8 MFMA tiles of 16x16.
 //   MFMA operand "A" (16 rows) = weights, operand "B" (16 cols) = activations.
-// Pipeline: a 4-deep LDS ring of stages (16 KiB each for int4 weights). Both operands go
+// Pipeline: a 3-slot LDS ring of stages (16 KiB each for int4 weights, RING below). Both operands go
 //   HBM/L2 -> LDS with global_load_lds_dwordx4 (issued from inline asm: no VGPRs, no ds_write, and
-//   no compiler-inserted vmcnt drains) three stages ahead; one counted `s_waitcnt vmcnt` + barrier per
+//   no compiler-inserted vmcnt drains) two stages ahead; one counted `s_waitcnt vmcnt` + barrier per
 //   stage; the MFMA fragments of stage k+1 are read from LDS while the MFMAs of stage k run.
 //   int4 weights stay packed in LDS and are sign-extended after the ds_read_b64 fragment read
 //   (each unpacked fragment feeds 8 MFMAs).
