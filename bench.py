@@ -19,9 +19,10 @@ int8 MFMA rate; traffic = HBM bytes per launch from rocprofv3 PMC counters (prof
 written by tools/profile_fc1.sh) or null. `kernels` gives the same event timing for every hot kernel
 of the block (fused qkv+attention, proj, fc2, LayerNorm) with its algorithmic work, taken in a second,
 untimed pass of the same steps (so the timed region carries only fc1's events); `model_frac` is the
-whole forward's int8 GEMM ops / ms_per_step / peak. `parity_tie_resolved` (N = 1, after timing): the
-GPU forward on the reference's own weight codes with every quantizer boundary checked against the oracle
-(oracle/ties.py), the logits' distance once rounding ties resolve alike.
+whole forward's int8 GEMM ops / ms_per_step / peak. `parity` (N = 1, after timing, parity_report): on the
+seed-12345 b2 images, the untied distance to the oracle split into weight-code and activation-code sources, and
+the tie-resolved check (every quantizer boundary against the oracle's, oracle/ties.py) whose `pass` is the
+tests' criterion.
 cpu_baseline: the CPU oracle's fp32 fake-quant forward (the reference's op sequence restated,
 oracle/quant_oracle.py) on a bounded sample of the same workload, rank 0 only, N = 1 only, with as
 many intra-op threads as this process may run on (affinity, capped by a cgroup CPU quota).
@@ -175,33 +176,72 @@ def cpu_baseline(model, model_name: str, x_gpu_logits_fn, img_size: int, batch: 
     }, rel, floor
 
 
-def tie_resolved_parity(model, model_name: str, img_size: int, dev) -> dict:
-    """After the timed region: the reference's own weight codes bound to the model (identical int4 weights),
-    then the GPU forward's every quantizer boundary against the oracle's (oracle/ties.py). Every differing
-    code must be a proven rounding tie; with ties resolved alike, `rel` is the logits' distance."""
+PARITY_SEED = 12345   # the bench's parity images (tests/test_gpu_bench_parity.py checks the same ones)
+PARITY_BATCH = 2
+
+
+def parity_report(model, model_name: str, img_size: int, dev) -> dict:
+    """After the timed region, on the bench's own b2 parity images (seed 12345):
+
+    * `untied`: the logits' distance to the oracle with nothing shared, split by source:
+      `rel_device_weights` (the timed configuration: the device's own weight codes), `weight_code_flips` (device
+      weight codes that differ from the oracle's, and how many of those the correctly rounded quantizer
+      explains, oracle/ties.py:cr_codes), `rel_oracle_weights` (the oracle's weight codes bound: what remains is
+      the activation codes' contribution), `floor_fp32_vs_fp64` (the oracle against itself in fp64).
+    * `tie_resolved`: with the oracle's weight codes bound, every quantizer boundary of the GPU forward against
+      the oracle's (oracle/ties.py). A differing code must be a proven rounding tie, and no layer may flip more
+      than the tests' 1e-4 budget of its codes; with ties resolved alike `rel` is the logits' distance. `pass`
+      is exactly the tests' criterion (tests/test_gpu_bench_parity.py)."""
     from oracle import quant_oracle as O
-    from oracle.ties import load_oracle_weight_codes, tie_resolved_vit_check
+    from oracle.ties import cr_codes, load_oracle_weight_codes, oracle_weight_codes, tie_resolved_vit_check
     from quantized_vit_amd.calibrate import VIT_CONFIGS, synthetic_images
+    from quantized_vit_amd.quant_layers import QuantizeMixin
     mc = VIT_CONFIGS[model_name]
     cfg = O.ViTConfig(img_size=mc["img_size"], patch_size=mc["patch_size"], embed_dim=mc["embed_dim"],
                       depth=mc["depth"], num_heads=mc["num_heads"])
-    load_oracle_weight_codes(model, cfg)
-    r = tie_resolved_vit_check(model, cfg, synthetic_images(2, img_size, seed=12345), dev)
+    img = synthetic_images(PARITY_BATCH, img_size, seed=PARITY_SEED)
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+
+    def rel(a, b):
+        return ((a.double() - b.double()).norm() / b.double().norm()).item()
+    with torch.no_grad():
+        ref = O.vit_forward(sd, cfg, img)
+        ref64 = O.vit_forward({k: v.double() for k, v in sd.items()}, cfg, img.double())
+        y_dev = model(img.to(dev)).cpu()
+        wflips, wcr, wtot, wlayers = 0, 0, 0, {}
+        for name, m in model.named_modules():
+            if not isinstance(m, QuantizeMixin):
+                continue
+            q = O.LayerQ.from_state(sd, name + ".", cfg.quant_type, cfg.quant_mode)
+            own = oracle_weight_codes(sd, name, cfg.quant_type, cfg.quant_mode).float()
+            got = m.weight_codes().cpu().reshape(own.shape)
+            diff = got != own
+            n = int(diff.sum())
+            wtot += own.numel()
+            if n:
+                w = sd[name + ".weight"].reshape(own.shape)[diff]
+                c = int((cr_codes(w, cfg.quant_type, q.d_wt, q.q_m_wt, q.t_wt) == got[diff]).sum())
+                wflips, wcr = wflips + n, wcr + c
+                wlayers[name] = {"flips": n, "cr_explained": c}
+        load_oracle_weight_codes(model, cfg)
+        y_ow = model(img.to(dev)).cpu()
+    untied = {"rel_device_weights": rel(y_dev, ref), "rel_oracle_weights": rel(y_ow, ref),
+              "floor_fp32_vs_fp64": rel(ref, ref64),
+              "weight_code_flips": {"flips": wflips, "cr_explained": wcr, "codes": wtot, "layers": wlayers}}
+    r = tie_resolved_vit_check(model, cfg, img, dev)
     non_ties = sum(s.get("non_ties", 0) for s in r["stats"].values())
     missing = list(r["missing"])
-    bad = [p for p, s in r["stats"].items() if s.get("non_ties", 0) > 0]
-    # layers whose proven ties exceed the 1e-4 flip budget of the tests (oracle/ties.py): reported with their
-    # largest tie distance. A dense cluster of values on one rounding boundary (e.g. fc2's input near the
-    # flat minimum of GELU, where many pre-activations give the same output) turns ulp-level differences of
-    # the two GELU evaluations into many ties; none of them is a non-tie difference.
-    dense = {p: {"flips": s["flips"], "total": s["total"], "max_tie_dist_code_units": s["max_dist"]}
-             for p, s in r["stats"].items() if p in r["bad"] and s.get("non_ties", 0) == 0}
-    return {"rel": r["rel"], "tie_flips": r["flips"], "codes": r["codes"], "non_tie_differences": non_ties,
-            "missing_layers": missing, "bad_layers": bad, "tie_dense_layers": dense,
-            "pass": bool(not missing and not bad and non_ties == 0 and r["rel"] <= 1e-3),
-            "batch": 2, "bound": "north star 1e-3 on identical int4 weights",
-            "weights": "the oracle's weight codes bound to the model after the timed region (the timed steps ran "
-                       "the device-derived codes; test_device_weight_codes_vs_reference pins those per code)"}
+    over = {p: {"flips": s["flips"], "total": s["total"], "cr_explained": s.get("cr_explained", 0),
+                "max_tie_dist_code_units": s["max_dist"]} for p, s in r["bad"].items()}
+    flipped = {p: {"flips": s["flips"], "cr_explained": s.get("cr_explained", 0)}
+               for p, s in r["stats"].items() if s.get("flips", 0)}
+    tied = {"rel": r["rel"], "tie_flips": r["flips"], "cr_explained": r["cr_explained"], "codes": r["codes"],
+            "non_tie_differences": non_ties, "missing_layers": missing, "layers_over_budget": over,
+            "flips_by_layer": flipped,
+            "pass": bool(not missing and not r["bad"] and non_ties == 0 and r["rel"] <= 1e-3),
+            "bound": "north star 1e-3 on identical int4 weights; every flip a proven tie; <= 1e-4 flips per layer"}
+    return {"batch": PARITY_BATCH, "seed": PARITY_SEED, "untied": untied, "tie_resolved": tied,
+            "weights": "device-derived weight codes in the timed steps; the oracle's bound after them"}
 
 
 def model_gemm_ops(model, B: int) -> float:
@@ -421,7 +461,7 @@ def main():
         result["cpu_baseline"] = cb
         result["parity_rel_err_vs_oracle"] = rel
         result["parity_oracle_fp32_vs_fp64"] = floor
-        result["parity_tie_resolved"] = tie_resolved_parity(model, args.model, img_size, dev)
+        result["parity"] = parity_report(model, args.model, img_size, dev)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

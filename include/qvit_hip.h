@@ -120,6 +120,13 @@ int qvit_fake_quant_f32(const float* x, int64_t n, int qtype, const float* d_qua
                         hipStream_t stream);
 
 /*
+ * y = GELU(x) elementwise over n contiguous floats: nn.GELU() (QViT_with_GETA/vit_model.py:173,242), bit-identical
+ * to torch's ATen CPU kernel (erf as Abramowitz-Stegun 7.1.26 with SLEEF's expf, IEEE division) — the same
+ * function the QVIT_EPI_I8_GELU epilogue evaluates. For the Mlp path outside the fused block, and for tests.
+ */
+int qvit_gelu_f32(const float* x, int64_t n, float* y, hipStream_t stream);
+
+/*
  * Weight quantizer + GEMM operand packing (QuantizeMixin.quantize_weight, quant_layers.py:332-354).
  *   w      : fp32 [n][ldw], first k columns used (nn.Linear weight [out,in]; a conv weight
  *            [Cout,Cin,kh,kw] is passed as [Cout][Cin*kh*kw]).
@@ -216,9 +223,9 @@ int qvit_gemm_wonly(const float* X, int64_t M, int64_t K, int64_t ldx, const voi
  *   gamma, beta, eps, out_* , ln_table : the LayerNorm and the next quantizer, as qvit_layernorm_quant_i8
  *              (ln_table: its QVIT_EPI_I8 code table, nullable; used if valid and <= 2174 buckets).
  *   codes    : int8 [M][ldcodes], the LayerNorm codes of the updated rows, columns [N, kpad_codes) zero.
- *   counters : int32 [ceil(M / 128)] (one per 128-row block), zero when first allocated and
- *              used by launches of one npad only, one launch at a time (stream order): each launch adds
- *              npad / 256 to every row block's counter, so the buffer is never reset.
+ *   counters : int32 [ceil(M / 128)] (one per 128-row block), scratch: the call zeroes it on `stream` before
+ *              the launch, so no state carries over between launches; it must not be shared with a launch
+ *              running concurrently on another stream.
  * The last of a row block's npad / 256 workgroups runs the LayerNorm of its rows; the residual rows are written
  * through (sc1) and read back with sc1 loads behind an agent-scope counter.
  */

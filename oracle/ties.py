@@ -37,19 +37,42 @@ def code_position(x: torch.Tensor, q_type: str, d: float, t: float) -> torch.Ten
     return p / d
 
 
+def cr_codes(x: torch.Tensor, q_type: str, d: float, q_m: float, t: float) -> torch.Tensor:
+    """The same quantizer with correctly rounded fp32 log and exp (each evaluated in fp64 and rounded once to
+    fp32) in place of torch's CPU ones (MKL VML: within 1 ulp, not correctly rounded; on ~1.5 % of inputs
+    exp(log(a)) differs from the correctly rounded composition, measured). This is the device's careful path
+    (csrc/qvit_common.h: code_mag_careful). Classifier only: a flip whose code equals this one comes from the
+    CPU's transcendental functions alone, not from any difference in the value being quantized."""
+    if q_type in (O.LINEAR, O.DGE):
+        return O.quant_codes(x, q_type, d, q_m, t)
+    x = x.float()
+    d32 = torch.tensor([d], dtype=torch.float32)
+    t32 = torch.tensor([t], dtype=torch.float32)
+    ax = x.abs()
+    pw = torch.exp((t32 * torch.log(ax.double()).float()).double()).float()
+    k = torch.round(pw / d32)
+    L = O.quant_codes(torch.tensor([abs(q_m) * 2 + 1.0]), q_type, d, q_m, t).abs()
+    k = torch.where(ax >= torch.tensor([q_m], dtype=torch.float32), L, k)
+    k = torch.where(ax <= 0, torch.zeros_like(k), k)
+    return torch.sign(x) * k
+
+
 def tie_check(x: torch.Tensor, got: torch.Tensor, own: torch.Tensor, q_type: str, d: float, q_m: float,
               t: float) -> dict:
     """Compares codes `got` with the reference's own codes `own` of the values `x` (same shapes).
     Returns counts: flips (differing codes), non_ties (differences that are not one-step rounding
-    ties), max_dist (largest tie distance from its boundary, code units)."""
+    ties), max_dist (largest tie distance from its boundary, code units), cr_explained (flips where the
+    quantizer with correctly rounded log/exp, cr_codes, gives `got` on the oracle's own value: the flip comes
+    from the CPU's exp/log alone)."""
     got = got.reshape(own.shape).to(own.dtype)
     diff = (got - own)
     idx = diff != 0
     n = int(idx.sum())
-    out = {"flips": n, "non_ties": 0, "max_dist": 0.0, "total": own.numel()}
+    out = {"flips": n, "non_ties": 0, "max_dist": 0.0, "total": own.numel(), "cr_explained": 0}
     if n == 0:
         return out
     xs, g, o = x.reshape(own.shape)[idx], got[idx], own[idx]
+    out["cr_explained"] = int((cr_codes(xs, q_type, d, q_m, t).to(g.dtype) == g).sum())
     one_step = (g - o).abs() == 1
     same_side = (g * o) >= 0                      # no sign change, except through 0
     kmin = torch.minimum(g.abs(), o.abs()).double()
@@ -148,4 +171,5 @@ def tie_resolved_vit_check(model, cfg, img, dev, flip_budget: float = 1e-4) -> d
            (s["non_ties"] > 0 or s["flips"] > max(1, flip_budget * s["total"]))}
     return {"rel": rel, "stats": hook.stats, "missing": missing, "bad": bad,
             "flips": sum(s.get("flips", 0) for s in hook.stats.values()),
+            "cr_explained": sum(s.get("cr_explained", 0) for s in hook.stats.values()),
             "codes": sum(s.get("total", 0) for s in hook.stats.values())}

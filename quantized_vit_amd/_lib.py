@@ -56,6 +56,7 @@ _f32 = ctypes.c_float
 _SIGNATURES = {
     "qvit_quantize_act_i8": [_c_p, _i64, _i64, _i64, _i32, _c_p, _c_p, _c_p, _i32, _c_p, _i64, _i64, _c_p],
     "qvit_fake_quant_f32": [_c_p, _i64, _i32, _c_p, _c_p, _c_p, _i32, _c_p, _c_p],
+    "qvit_gelu_f32": [_c_p, _i64, _c_p, _c_p],
     "qvit_pack_weight": [_c_p, _i64, _i64, _i64, _i32, _c_p, _c_p, _c_p, _i32, _c_p, _i64, _i64, _c_p, _c_p],
     "qvit_pad_bias": [_c_p, _i64, _c_p, _i64, _c_p],
     "qvit_im2col_quant_i8": [_c_p, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32,
@@ -125,10 +126,19 @@ def version() -> str:
 
 
 def build_id(path: Optional[str] = None) -> Optional[str]:
-    """Identity of a library build (sha256 prefix of the .so file): profile JSONs record the build they
-    were measured on, and bench.py merges their counters only into a line timed on that same build."""
+    """Identity of a library build: the digest of its build inputs (sources, headers, build script, flags and
+    defines; build.py writes it beside the library as <lib>.srcsha), so a rebuild from the same inputs keeps its
+    id. Profile JSONs record the build they were measured on, and bench.py merges their counters
+    only into a line timed on that same build. A library without a digest file falls back to its bytes' sha256."""
     import hashlib
     p = path or (getattr(_lib, "_name", None) if _lib is not None else None) or LIB_PATH
+    try:
+        with open(p + ".srcsha") as f:
+            digest = f.read().strip()
+        if digest:
+            return "src-" + digest[:16]
+    except OSError:
+        pass
     try:
         with open(p, "rb") as f:
             return hashlib.sha256(f.read()).hexdigest()[:16]
@@ -174,6 +184,15 @@ def fake_quant_f32(x: torch.Tensor, qtype: int, d: Optional[torch.Tensor], qm: O
     y = torch.empty_like(xc)
     _check(load().qvit_fake_quant_f32(_ptr(xc), xc.numel(), qtype, _ptr(d), _ptr(qm), _ptr(t), levels, _ptr(y),
                                       _stream(x.device)), "qvit_fake_quant_f32")
+    return y
+
+
+def gelu_f32(x: torch.Tensor) -> torch.Tensor:
+    """nn.GELU() bit-identical to torch's ATen CPU kernel (qvit_gelu_f32)."""
+    _require_gpu(x, "input")
+    xc = x.contiguous().float()
+    y = torch.empty_like(xc)
+    _check(load().qvit_gelu_f32(_ptr(xc), xc.numel(), _ptr(y), _stream(x.device)), "qvit_gelu_f32")
     return y
 
 
@@ -259,18 +278,15 @@ def gemm(A: torch.Tensor, M: int, K: int, packed: torch.Tensor, wfmt: int, N: in
     return C
 
 
-_WONLY_WS: dict = {}
-WONLY_WS_MAX = 64 << 20   # bytes of split-K partials kept per device (small-M weight-only layers)
+WONLY_WS_MAX = 64 << 20   # bytes of split-K partials per call (small-M weight-only layers)
 
 
 def wonly_workspace(device: torch.device, M: int, npad: int) -> Optional[torch.Tensor]:
-    """Split-K workspace of qvit_gemm_wonly for M rows (at most 256 partial sets), one buffer per device."""
+    """Split-K workspace of qvit_gemm_wonly for M rows (at most 256 partial sets). A fresh buffer per call from
+    torch's caching allocator, which ties it to the current stream: launches on different streams never share
+    partials."""
     need = min(256 * M * npad * 4, WONLY_WS_MAX)
-    buf = _WONLY_WS.get(str(device))
-    if buf is None or buf.numel() * 4 < need:
-        buf = torch.empty(need // 4 + 4, dtype=torch.float32, device=device)
-        _WONLY_WS[str(device)] = buf
-    return buf
+    return torch.empty(need // 4 + 4, dtype=torch.float32, device=device)
 
 
 def gemm_wonly(X: torch.Tensor, M: int, K: int, packed: torch.Tensor, wfmt: int, N: int, npad: int,
@@ -286,19 +302,10 @@ def gemm_wonly(X: torch.Tensor, M: int, K: int, packed: torch.Tensor, wfmt: int,
     return Y
 
 
-_LN_COUNTERS: dict = {}
-
-
 def resid_ln_counters(device: torch.device, rows: int, npad: int) -> torch.Tensor:
-    """Arrival counters of qvit_gemm_resid_ln for `rows` rows: one zero-initialised int32 per 128-row block,
-    one buffer per (device, npad) (each launch adds npad / 256 per block, so a buffer serves one npad)."""
-    key = (str(device), npad)
-    need = (rows + 127) // 128
-    buf = _LN_COUNTERS.get(key)
-    if buf is None or buf.numel() < need:
-        buf = torch.zeros(max(need, 1), dtype=torch.int32, device=device)
-        _LN_COUNTERS[key] = buf
-    return buf
+    """Arrival counters of qvit_gemm_resid_ln for `rows` rows: one int32 per 128-row block. The call zeroes them
+    on its stream; a fresh buffer per call (caching allocator, stream-bound) so concurrent launches never share."""
+    return torch.empty(max((rows + 127) // 128, 1), dtype=torch.int32, device=device)
 
 
 def gemm_resid_ln(A: torch.Tensor, M: int, K: int, packed: torch.Tensor, wfmt: int, N: int, npad: int,

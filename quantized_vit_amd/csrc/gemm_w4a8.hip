@@ -118,7 +118,7 @@ struct EpiArgs {
   int8_t* ln_codes;
   int64_t ln_ldc;
   int ln_kpad;
-  int* ln_cnt;             // arrivals per 128-row block (monotone: npad / 256 per launch)
+  int* ln_cnt;             // arrivals per 128-row block (zeroed by qvit_gemm_resid_ln before the launch)
 };
 
 // ---- code table of the int8 epilogues --------------------------------------------------------------
@@ -377,7 +377,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     asm volatile("s_barrier" ::: "memory");
     if (tid == 0) {
       const int old = __hip_atomic_fetch_add(ep.ln_cnt + m0 / BM, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *flag = (old % nb_n) == nb_n - 1 ? 1 : 0;
+      *flag = old == nb_n - 1 ? 1 : 0;  // counters zeroed by the launcher
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);
     asm volatile("s_barrier" ::: "memory");
@@ -975,6 +975,9 @@ extern "C" int qvit_gemm_resid_ln(const int8_t* A, int64_t M, int64_t K, int64_t
   if (q != QVIT_QT_LINEAR && q != QVIT_QT_NONLINEAR && q != QVIT_QT_ULTRA_ACT) return QVIT_EINVAL;
   if (q == QVIT_QT_ULTRA_ACT ? (out_levels < 1 || out_levels > 127) : (!out_d || !out_qm)) return QVIT_EINVAL;
   if (M == 0) return QVIT_OK;
+  // fresh arrival counters for this launch (the hand-off never depends on earlier launches)
+  const hipError_t ez = hipMemsetAsync(counters, 0, (size_t)((M + 127) / 128) * sizeof(int32_t), stream);
+  if (ez != hipSuccess) return qvit_hip_status(ez);
   EpiArgs ep{d_act, d_wt, bias, out_qtype, out_d, out_qm, out_t, out_levels, nullptr, 1, 1.f, 1.f, nullptr,
              gamma, beta, eps, reinterpret_cast<const int8_t*>(ln_table), codes, ldcodes, (int)kpad_codes,
              reinterpret_cast<int*>(counters)};

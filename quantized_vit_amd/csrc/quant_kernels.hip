@@ -71,6 +71,11 @@ __global__ __launch_bounds__(kThreads) void fake_quant_kernel(const float* __res
   }
 }
 
+__global__ __launch_bounds__(kThreads) void gelu_kernel(const float* __restrict__ x, int64_t n, float* __restrict__ y) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = gelu_ref(x[i]);
+}
+
 // ---- weight quantizer + operand packing ------------------------------------------------------
 // Packed row rho holds weight row perm(rho): inside each 64-row group swap bits [3:2] and [5:4].
 __device__ __forceinline__ int64_t perm_row(int64_t rho) {
@@ -451,6 +456,14 @@ int qvit_fake_quant_f32(const float* x, int64_t n, int qtype, const float* d_qua
   if (n == 0) return QVIT_OK;
   hipLaunchKernelGGL(fake_quant_kernel, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, stream, x,
                      n, qtype, d_quant, q_m, t_quant, levels, y);
+  return qvit_hip_status(hipGetLastError());
+}
+
+int qvit_gelu_f32(const float* x, int64_t n, float* y, hipStream_t stream) {
+  if (!x || !y) return QVIT_ENULL;
+  if (n < 0) return QVIT_EINVAL;
+  if (n == 0) return QVIT_OK;
+  hipLaunchKernelGGL(gelu_kernel, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, stream, x, n, y);
   return qvit_hip_status(hipGetLastError());
 }
 

@@ -182,18 +182,48 @@ QVIT_DEV void epi_select_byte(uint32_t& wd, float v, float thr, uint32_t lohi) {
 }
 
 
-// nn.GELU() (approximate='none', vit_model.py:242,173) as the reference computes it on the CPU:
-// x * 0.5 * (1 + erf(x * M_SQRT1_2)) with torch's vectorized erf = Abramowitz-Stegun 7.1.26
-// (ATen/cpu/vec/vec512/vec512_float.h, Vectorized<float>::erf): sign(u) * (1 - r(t) t exp(-u^2)),
-// t = 1 / (1 + 0.3275911 |u|). Branch-free, one exp. (|erf error| <= 1.5e-7, like the reference.)
+// SLEEF's single-precision exp, 1-ulp variant (Sleef_expf*_u10, the `xexpf` kernel torch links statically):
+// Cody-Waite reduction by ln 2 in two fp32 parts, a degree-6 polynomial in fma steps, and the scale by 2^q
+// as two power-of-two multiplies. Every step is one IEEE fp32 operation, so the device value equals the
+// CPU's bit for bit (pinned by tests/test_gpu_kats.py::test_gelu_bit_exact_all_floats).
+QVIT_DEV float pow2i_f(int q) { return __int_as_float((q + 0x7f) << 23); }
+QVIT_DEV float sleef_expf_u10(float d) {
+#pragma clang fp contract(off)
+  // q = rint(d / ln 2), clamped only where the result is overridden below (|d| > 104)
+  const float fq = fminf(fmaxf(rintf(d * 1.442695040888963407359924681001892137426645954152985934135449406931f),
+                               -256.f), 256.f);
+  const int q = (int)fq;
+  float s = fmaf(fq, -0.693145751953125f, d);
+  s = fmaf(fq, -1.428606765330187045e-06f, s);
+  float u = 0.000198527617612853646278381f;
+  u = fmaf(u, s, 0.00139304355252534151077271f);
+  u = fmaf(u, s, 0.00833336077630519866943359f);
+  u = fmaf(u, s, 0.0416664853692054748535156f);
+  u = fmaf(u, s, 0.166666671633720397949219f);
+  u = fmaf(u, s, 0.5f);
+  u = 1.0f + fmaf(s * s, u, s);
+  u = (u * pow2i_f(q >> 1)) * pow2i_f(q - (q >> 1));
+  u = (d < -104.f) ? 0.f : u;
+  return (d > 100.f) ? INFINITY : u;
+}
+
+// nn.GELU() (approximate='none', vit_model.py:242,173) exactly as torch's ATen CPU kernel computes it
+// (GeluKernelImpl, vectorized branch): (x * 0.5) * (1 + erf(x * M_SQRT1_2)) with Vectorized<float>::erf =
+// Abramowitz-Stegun 7.1.26: sign(u) * fma(-exp(-u*u) * t, r(t), 1), t = 1 / fma(0.3275911, |u|, 1) (IEEE
+// division), r a degree-4 Horner polynomial in fma steps, exp = SLEEF expf u10. Bit-identical to the oracle's
+// GELU (oracle/quant_oracle.py:gelu) on every fp32 input. Used by the int8-epilogue code tables and the
+// direct epilogue; the per-element cost is irrelevant there (the tables are built once per quantizer).
 QVIT_DEV float gelu_ref(float x) {
-  const float u = x * 0.70710678f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, fabsf(u), 1.0f));
-  const float r = fmaf(fmaf(fmaf(fmaf(1.061405429f, t, -1.453152027f), t, 1.421413741f), t, -0.284496736f), t,
-                       0.254829592f);
-  const float e = __expf(-(u * u));
+#pragma clang fp contract(off)
+  const float u = x * 0.70710678118654752440f;
+  const float t = 1.0f / fmaf(0.3275911f, fabsf(u), 1.0f);
+  float r = fmaf(1.061405429f, t, -1.453152027f);
+  r = fmaf(r, t, 1.421413741f);
+  r = fmaf(r, t, -0.284496736f);
+  r = fmaf(r, t, 0.254829592f);
+  const float e = sleef_expf_u10(-(u * u));
   const float erf_abs = fmaf(-e * t, r, 1.0f);
-  return x * 0.5f * (1.0f + copysignf(erf_abs, u));
+  return (x * 0.5f) * (1.0f + copysignf(erf_abs, u));
 }
 
 // ---- LDS-DMA and asm-issued global loads (GEMM and fused-attention pipelines) ------------------------

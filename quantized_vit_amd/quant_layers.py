@@ -344,8 +344,10 @@ class QuantizeMixin:
         if plan.int_path or plan.extra.get("wonly"):
             bias = self.bias.detach() if self.bias is not None else None
             plan.bias_pad = _lib.pad_bias(bias, n, npad, dev)
-            # |output| <= d_act d_wt sum_k |a_k||w_k| + |bias| <= d_act d_wt K L_a L_w + max|bias|
-            plan.extra["out_bound"] = abs(s[3] * s[0]) * k * abs(la) * abs(lw) + s[-1]
+            # |output| <= d_act d_wt sum_k |a_k||w_k| + |bias| <= d_act d_wt K L_a L_w + max|bias| (integer path
+            # only: a weight-only plan has no activation scalars, and its output is unbounded a priori)
+            plan.extra["out_bound"] = (abs(s[3] * s[0]) * k * abs(la) * abs(lw) + s[-1]) if plan.int_path \
+                else float("inf")
         if wa:   # host copies of the activation quantizer's scalars (epilogue code tables of the producer)
             plan.extra["act_host"] = (qt, s[3], s[4], s[5] if t_act is not None else 1.0, la)
         if not plan.int_path and not plan.extra.get("wonly"):   # levels that fit neither int4 nor int8 (e.g. 16/32
@@ -434,6 +436,7 @@ class QuantizeMixin:
 
 
 _GELU_MAX_SLOPE = 1.1289   # max of d/dv [v Phi(v)] (at v ~ 1.41)
+WONLY_CONV_BYTES = 1 << 30  # patch-row bytes per chunk of a weight-only QuantizeConv2d
 
 
 def _gelu(v: float) -> float:
@@ -628,14 +631,22 @@ class QuantizeConv2d(nn.Conv2d, QuantizeMixin):
             # weight-only / wide levels: the input patches (K order (c, kh, kw) = the weight flattening) as fp32
             # rows against the packed codes (qvit_gemm_wonly)
             B = x.shape[0]
-            cols = F.unfold(x.detach(), self.kernel_size, self.dilation, self.padding, self.stride)  # [B, K, L]
-            L = cols.shape[2]
             OH = (x.shape[2] + 2 * self.padding[0] - self.dilation[0] * (self.kernel_size[0] - 1) - 1) // self.stride[0] + 1
-            OW = L // OH
-            x2 = torch.zeros((B * L, plan.kpad), dtype=torch.float32, device=x.device)
-            x2.view(B, L, plan.kpad)[:, :, :plan.k] = cols.transpose(1, 2)
-            y = self._wonly_rows(x2, plan)
-            return y.reshape(B, OH, OW, plan.n).permute(0, 3, 1, 2).contiguous()
+            OW = (x.shape[3] + 2 * self.padding[1] - self.dilation[1] * (self.kernel_size[1] - 1) - 1) // self.stride[1] + 1
+            L = OH * OW
+            # images in chunks whose patch rows stay within a byte budget (a 3x3 conv at 416 x 416 and B = 256
+            # would otherwise materialise ~22 GB of zero-padded fp32 rows)
+            per_img = L * plan.kpad * 4 * 2
+            step = max(1, min(B, WONLY_CONV_BYTES // max(per_img, 1)))
+            y = torch.empty((B, L, plan.n), dtype=torch.float32, device=x.device)
+            for b0 in range(0, B, step):
+                xb = x.detach()[b0:b0 + step]
+                cols = F.unfold(xb, self.kernel_size, self.dilation, self.padding, self.stride)  # [b, K, L]
+                x2 = torch.zeros((xb.shape[0] * L, plan.kpad), dtype=torch.float32, device=x.device)
+                x2.view(xb.shape[0], L, plan.kpad)[:, :, :plan.k] = cols.transpose(1, 2)
+                del cols
+                y[b0:b0 + step] = self._wonly_rows(x2, plan).view(xb.shape[0], L, plan.n)
+            return y.view(B, OH, OW, plan.n).permute(0, 3, 1, 2).contiguous()
         w = self.w_fakequant(plan).view_as(self.weight)
         return F.conv2d(x.detach(), w, None if self.bias is None else self.bias.detach(), self.stride,
                         self.padding, self.dilation, self.groups)
