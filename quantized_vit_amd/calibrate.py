@@ -67,6 +67,34 @@ def set_weight_quant_t(model: nn.Module, t: float, bits: int = 4) -> None:
             mod.invalidate()
 
 
+@torch.no_grad()
+def redraw_init_artifacts(model: nn.Module, limit: float = 1.0) -> int:
+    """Re-draws the sampling artifacts of torch.nn.init.trunc_normal_ in a freshly initialised ViT.
+
+    _init_vit_weights (vit_model.py:331-346) draws Linear weights from trunc_normal_(std=.01) and the class / position
+    embeddings from trunc_normal_(std=.02), truncated at the absolute bounds [-2, 2] (200 / 100 sigma). torch samples it
+    by inverse CDF: uniform_(-1, 1) then erfinv_; a uniform draw of exactly -1 (about 2^-24 per element) becomes -inf and
+    is clamped to -2.0. So a ViT-L/16 holds a dozen weights of exactly +-2.0 (12 layers at seed 0, the head among
+    them), values the intended distribution gives with probability ~0. Under the per-tensor max quantizer
+    (initialize_quant_layer: d = max|W| / 7) such a layer's int4 codes are all 0 but one: the head then has one
+    nonzero weight, the logits depend on a single activation code per image, and any logits comparison becomes a coin
+    toss on that code's rounding. Every element with |w| >= `limit` (50-100 sigma) is re-drawn from the intended
+    normal with the global generator (deterministic for a seed; a model without artifacts is left unchanged).
+    Returns the number of elements re-drawn."""
+    n = 0
+    for name, p in model.named_parameters():
+        std = 0.02 if name in ("pos_embed", "cls_token", "dist_token") else 0.01
+        if not (name.endswith("weight") and p.dim() == 2) and std == 0.01:
+            continue
+        mask = p.abs() >= limit
+        while bool(mask.any()):
+            k = int(mask.sum())
+            n += k
+            p[mask] = torch.randn(k) * std
+            mask = p.abs() >= limit
+    return n
+
+
 VIT_CONFIGS = {
     "vit_tiny_patch16_224": dict(img_size=224, patch_size=16, embed_dim=192, depth=12, num_heads=3),
     "vit_base_patch16_224": dict(img_size=224, patch_size=16, embed_dim=768, depth=12, num_heads=12),
@@ -90,6 +118,7 @@ def build_quantized_vit(name: str = "vit_base_patch16_224", num_classes: int = 1
         cfg["depth"] = depth
     g = torch.manual_seed(seed)
     model = vit_model.VisionTransformer(num_classes=num_classes, representation_size=None, **cfg)
+    redraw_init_artifacts(model)
     dev = device or torch.device("cpu")
     model = model.to(dev).eval()
     gen = torch.Generator(device="cpu").manual_seed(calib_seed)

@@ -79,13 +79,6 @@ struct Geo {
 QVIT_DEV uint32_t nib16_lo(uint32_t p) { return (p << 4) & 0xF0F0F0F0u; }
 QVIT_DEV uint32_t nib16_hi(uint32_t p) { return p & 0xF0F0F0F0u; }
 
-// Lane id from a volatile asm: values derived from it are recomputed where used instead of being
-// hoisted out of the tile loop (which would keep them live across the register-bound main loop).
-QVIT_DEV int lane_opaque() {
-  int l;
-  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-  return l;
-}
 
 // Wait until at most N of this wave's DMAs are in flight, retire its LDS reads, then barrier.
 // The LDS drain is the builtin (lgkmcnt(0) = 0xC07F on gfx9) so the compiler's wait-count model sees

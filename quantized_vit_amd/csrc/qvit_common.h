@@ -129,6 +129,7 @@ QVIT_DEV int8_t to_i8_sat(float k) {
   return (int8_t)(int)k;
 }
 
+
 // ---- code tables of the int8 epilogues (qvit_epi_table_build; GEMM and attention epilogues) ----------
 // header (16 B) + nb entries {thr, lo | hi << 8} (8 B each); see gemm_w4a8.hip for the construction.
 struct EpiTableHdr {
@@ -224,6 +225,14 @@ QVIT_DEV float gelu_ref(float x) {
   const float e = sleef_expf_u10(-(u * u));
   const float erf_abs = fmaf(-e * t, r, 1.0f);
   return (x * 0.5f) * (1.0f + copysignf(erf_abs, u));
+}
+
+// Lane id from a volatile asm: values derived from it are recomputed where used instead of being
+// hoisted out of the tile / unit loop (which would keep them live across the register-bound main loop).
+QVIT_DEV int lane_opaque() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
 }
 
 // ---- LDS-DMA and asm-issued global loads (GEMM and fused-attention pipelines) ------------------------

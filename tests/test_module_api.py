@@ -125,3 +125,23 @@ def test_ultranet_cpu_forward_fails_loudly():
     m = UltraNetQua().eval()
     with pytest.raises(_lib.QvitError):
         m(torch.rand(1, 3, 64, 64))
+
+
+def test_trunc_normal_artifacts_redrawn():
+    """torch's trunc_normal_(std=.01, a=-2, b=2) turns a uniform draw of exactly -1 into -2.0 (inverse CDF at -inf,
+    clamped): ViT-L/16 at seed 0 gets twelve +-2.0 weights, which make those layers' int4 codes all zero but one under
+    the per-tensor max quantizer. calibrate.redraw_init_artifacts re-draws exactly those elements; ViT-B/16 at seed 0
+    has none and is left bit-identical."""
+    import torch
+    from quantized_vit_amd import vit_model
+    from quantized_vit_amd.calibrate import VIT_CONFIGS, redraw_init_artifacts
+    torch.manual_seed(0)
+    vl = vit_model.VisionTransformer(num_classes=1000, representation_size=None, **VIT_CONFIGS["vit_large_patch16_384"])
+    assert float(vl.head.weight.abs().max()) == 2.0
+    assert redraw_init_artifacts(vl) >= 12
+    assert max(float(p.abs().max()) for n, p in vl.named_parameters() if p.dim() == 2) < 0.1
+    torch.manual_seed(0)
+    vb = vit_model.VisionTransformer(num_classes=1000, representation_size=None, **VIT_CONFIGS["vit_base_patch16_224"])
+    before = {k: v.clone() for k, v in vb.state_dict().items()}
+    assert redraw_init_artifacts(vb) == 0
+    assert all(torch.equal(before[k], v) for k, v in vb.state_dict().items())

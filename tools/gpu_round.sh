@@ -20,4 +20,9 @@ for step in "$@"; do
     echo "== stopping: $name ended with status $rc"
     exit $rc
   fi
+  # a GPU fault inside a test shows up as an ordinary failure (rc 1): stop on its signature too
+  if grep -qE "illegal memory access|hipErrorIllegalAddress|Memory access fault|HSA_STATUS_ERROR|GPU Hang|hipErrorLaunchFailure" "$OUT/$name.log"; then
+    echo "== stopping: $name hit a GPU fault"
+    exit 3
+  fi
 done
