@@ -111,6 +111,14 @@ def yolo_decode(p: torch.Tensor, img_size) -> Tuple[torch.Tensor, torch.Tensor]:
     return io.view(bs, -1, no), p
 
 
+def ultranet_block(sd: Dict[str, torch.Tensor], k: int, x: torch.Tensor) -> torch.Tensor:
+    """Quantized block k of UltraNetQua.layers alone (mymodel.py:71-124): Conv2d_Q -> BatchNorm2d (eval) ->
+    activation_quantize_fn (-> MaxPool2d(2, 2) for k < 4), as ultranet_forward runs it. Values k/15."""
+    (cp, bp), (_, _, ks, pool) = layer_prefixes()[k], CONV_SPECS[k]
+    x = activation_quantize(batch_norm_eval(conv_q(x, sd[cp + ".weight"], None, 1, ks // 2), sd, bp))
+    return F.max_pool2d(x, 2, 2) if pool else x
+
+
 def ultranet_forward(sd: Dict[str, torch.Tensor], x: torch.Tensor, trace: list = None):
     """UltraNetQua.forward (mymodel.py:134-144), eval mode. Returns (io [B, na*ny*nx, 6], p).
     If `trace` is a list, the activation after every quantized block is appended (post act-quant,

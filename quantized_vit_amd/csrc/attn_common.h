@@ -65,11 +65,6 @@ QVIT_DEV float xsum(float v) {
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
-// Deferred running max in the online softmax (attend); 0: rescale at every key block (A/B builds).
-#ifndef QVIT_ATT_DEFER
-#define QVIT_ATT_DEFER 1
-#endif
-
 // Stamps (phase timing of diagnostic builds; empty in the library): diag_stamps.h.
 
 // Online-softmax update of one key block (KB keys in the LDS images at st) for a wave's first NT query
@@ -139,13 +134,10 @@ QVIT_DEV void attend(int nt, bool mask, const int8_t* st, const h8 (&qh)[T][2], 
     }
     float bm = fmax_nn(fmax_nn(fmax_nn(r[0], r[1]), fmax_nn(r[2], r[3])), fmax_nn(fmax_nn(r[4], r[5]), fmax_nn(r[6], r[7])));
     bm = xmax(bm) * sl2;
-#if QVIT_ATT_DEFER
     // deferred max: the running max moves only when some query's block max exceeds it by more than 8
     // (log2 units), so P <= 2^8 (exact in the fp16 hi/lo split) and o, l are rescaled only then; a query
     // whose max did not grow gets alpha = exp2(0) = 1 exactly
-    if (__builtin_amdgcn_ballot_w64(bm > m[i] + 8.f) != 0)
-#endif
-    {
+    if (__builtin_amdgcn_ballot_w64(bm > m[i] + 8.f) != 0) {
       const float mn = fmax_nn(m[i], bm);
       const float alpha = __builtin_amdgcn_exp2f(m[i] - mn);
       l[i] *= alpha;

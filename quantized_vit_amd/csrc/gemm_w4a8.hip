@@ -350,13 +350,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   auto step_core = [&](Frags<WFMT>& cur, Frags<WFMT>& nxt, int next_slot, bool read) __attribute__((always_inline)) {
     if (read) read_frags(next_slot, nxt);
     __builtin_amdgcn_sched_barrier(0);
-#if defined(QVIT_GEMM_PRIO)
-    __builtin_amdgcn_s_setprio(1);
-#endif
     mfma_stage(cur);
-#if defined(QVIT_GEMM_PRIO)
-    __builtin_amdgcn_s_setprio(0);
-#endif
     __builtin_amdgcn_sched_barrier(0);
   };
 
@@ -843,11 +837,7 @@ int device_cus() {
 template <int WFMT, int EPI>
 int launch(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int64_t N, int64_t npad,
            void* C, int64_t ldc, const EpiArgs& ep, hipStream_t stream) {
-#if defined(QVIT_GEMM_WM)
-  constexpr int WMV = (WFMT == QVIT_W4) ? QVIT_GEMM_WM : 1;
-#else
-  constexpr int WMV = 1;
-#endif
+  constexpr int WMV = 1;   // (a second W4 tile width was measured slower in round 3: DESIGN.md section 8)
   using G = Geo<WFMT, WMV>;
   // the kernel addresses A and Wp as 32-bit byte offsets from the base pointers: rows are launched in
   // chunks whose A span stays below 2^32 (one chunk for every ViT / UltraNet shape)

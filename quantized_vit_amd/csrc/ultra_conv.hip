@@ -142,14 +142,10 @@ QVIT_DEV _Float16 lo_h(float x) { return (_Float16)(x - (float)(_Float16)x); }  
 // patches per MFMA group and workgroups per CU of the layer-0 kernel: one patch at a time holds 64 VGPRs, so
 // LDS (23 KiB per workgroup) rather than registers bounds residency at 7 workgroups per CU; 4 patches per group
 // at 4 workgroups per CU (round-3 build): 344-353 us vs 283-286 us at b256 (profiles/r03_conv0_occupancy_ab.txt)
-#ifndef QVIT_C0_G
-#define QVIT_C0_G 1
-#endif
-#ifndef QVIT_C0_OCC
-#define QVIT_C0_OCC 6
-#endif
+constexpr int C0_G = 1;     // patches per MFMA group
+constexpr int C0_OCC = 6;   // workgroups per CU
 template <bool VEC>
-__global__ __launch_bounds__(256, QVIT_C0_OCC) void ultra_conv0_mfma_kernel(const float* __restrict__ img, int B, int H, int W,
+__global__ __launch_bounds__(256, C0_OCC) void ultra_conv0_mfma_kernel(const float* __restrict__ img, int B, int H, int W,
                                                                const float* __restrict__ wvals,
                                                                const float* __restrict__ alpha,
                                                                const float* __restrict__ shift, float levels,
@@ -245,18 +241,18 @@ __global__ __launch_bounds__(256, QVIT_C0_OCC) void ultra_conv0_mfma_kernel(cons
     const int8_t* r1 = g < 3 ? rec(g, 1) : rec(1, 2);
     const int8_t* c0 = rec(2, 2);
     const int8_t* c1 = rec(2, 2) + (g == 0 ? C0_PLANE : 0);
-    // QVIT_C0_G patches at a time (their MFMA chains interleaved; with one, the other resident waves cover the
+    // C0_G patches at a time (their MFMA chains interleaved; with one, the other resident waves cover the
     // chain latency)
 #pragma unroll
-    for (int pq = 0; pq < C0_TX / 4; pq += QVIT_C0_G) {
-      c0h8 h0[QVIT_C0_G], l0[QVIT_C0_G], x1[QVIT_C0_G];
-      c0f4 acc[QVIT_C0_G];
+    for (int pq = 0; pq < C0_TX / 4; pq += C0_G) {
+      c0h8 h0[C0_G], l0[C0_G], x1[C0_G];
+      c0f4 acc[C0_G];
       auto pair = [](const int8_t* a, const int8_t* b) {
         return __builtin_shufflevector(*reinterpret_cast<const c0h4*>(a), *reinterpret_cast<const c0h4*>(b), 0, 1, 2, 3,
                                        4, 5, 6, 7);
       };
 #pragma unroll
-      for (int q = 0; q < QVIT_C0_G; ++q) {
+      for (int q = 0; q < C0_G; ++q) {
         const int o = 32 * (pq + q);
         h0[q] = pair(r0 + o, r1 + o);
         l0[q] = pair(r0 + C0_PLANE + o, r1 + C0_PLANE + o);
@@ -264,16 +260,16 @@ __global__ __launch_bounds__(256, QVIT_C0_OCC) void ultra_conv0_mfma_kernel(cons
         acc[q] = c0f4{0.f, 0.f, 0.f, 0.f};
       }
 #pragma unroll
-      for (int q = 0; q < QVIT_C0_G; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(h0[q], wh0, acc[q], 0, 0, 0);
+      for (int q = 0; q < C0_G; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(h0[q], wh0, acc[q], 0, 0, 0);
 #pragma unroll
-      for (int q = 0; q < QVIT_C0_G; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(x1[q], wc1, acc[q], 0, 0, 0);
+      for (int q = 0; q < C0_G; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(x1[q], wc1, acc[q], 0, 0, 0);
 #pragma unroll
-      for (int q = 0; q < QVIT_C0_G; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(l0[q], wh0, acc[q], 0, 0, 0);
+      for (int q = 0; q < C0_G; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(l0[q], wh0, acc[q], 0, 0, 0);
 #pragma unroll
-      for (int q = 0; q < QVIT_C0_G; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(h0[q], wl0, acc[q], 0, 0, 0);
+      for (int q = 0; q < C0_G; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(h0[q], wl0, acc[q], 0, 0, 0);
       // acc[q][j] = conv[pixel 4 g + j of patch pq + q][channel n]: window g's four pixels
 #pragma unroll
-      for (int q = 0; q < QVIT_C0_G; ++q) {
+      for (int q = 0; q < C0_G; ++q) {
         const float mx = fmax_nn(fmax_nn(acc[q][0], acc[q][1]), fmax_nn(acc[q][2], acc[q][3]));
         const float mn = fmin_nn(fmin_nn(acc[q][0], acc[q][1]), fmin_nn(acc[q][2], acc[q][3]));
         const float y = __fadd_rn(__fmul_rn(up ? mx : mn, al), sh);
@@ -437,14 +433,9 @@ struct ConvGeo {
 //      2 = integer deploy threshold (alpha / shift hold int32 inc_q / bias_q, sbits = S; POOL as for 0)
 // minimum resident workgroups per CU by input width (register budget): CIN 32 at 3 instead of 2 (168 VGPRs, no
 // spills): conv2 114-116 -> 96-98 us at b256 (profiles/r03_conv0_occupancy_ab.txt)
-#ifndef QVIT_UC_MINB16
-#define QVIT_UC_MINB16 2
-#endif
-#ifndef QVIT_UC_MINB32
-#define QVIT_UC_MINB32 3
-#endif
+constexpr int UC_MINB16 = 2, UC_MINB32 = 3;
 template <int CIN, int KS, int COUT, int POOL, int OUT>
-__global__ __launch_bounds__(256, CIN == 32 ? QVIT_UC_MINB32 : CIN == 16 ? QVIT_UC_MINB16 : 2) void ultra_conv_kernel(const int8_t* __restrict__ in, int B, int H, int W,
+__global__ __launch_bounds__(256, CIN == 32 ? UC_MINB32 : CIN == 16 ? UC_MINB16 : 2) void ultra_conv_kernel(const int8_t* __restrict__ in, int B, int H, int W,
                                                             const int8_t* __restrict__ wcodes, int kpad_in,
                                                             float den, const float* __restrict__ alpha,
                                                             const float* __restrict__ shift, float levels,

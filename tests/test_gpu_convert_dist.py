@@ -112,3 +112,34 @@ def test_sharded_quantized_vit_two_ranks(dev, global_batch):
         # per-image work is independent of the batch it runs in; the head's library GEMM may pick another
         # kernel for another M, so allow fp32 rounding
         assert err <= 1e-5, (rank, err)
+
+
+def test_rccl_world1_all_gather_on_device(dev):
+    """RCCL itself (backend "nccl") on one rank: librccl loads, the communicator initialises on the device, and
+    all_gather_into_tensor moves device buffers, the collective distributed.gather_logits issues on the 8-GPU node
+    (configs[2]). The ragged-shard padding path of gather_logits is checked with a world-1 group as well."""
+    import torch.distributed as dist
+    from quantized_vit_amd import distributed as qd
+    assert not dist.is_initialized()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device(dev))
+    try:
+        assert dist.get_backend() == "nccl"
+        x = torch.randn(256, 1000, device=dev)
+        out = torch.empty_like(x)
+        dist.all_gather_into_tensor(out, x)
+        torch.cuda.synchronize()
+        assert torch.equal(out, x)
+        # a world-1 group through the module's collective path (world == 1 short-circuits the gather)
+        assert torch.equal(qd.gather_logits(x, 256), x)
+        y = torch.randn(5, 10, device=dev)
+        big = torch.empty(5, 10, device=dev)
+        dist.all_gather_into_tensor(big, y.contiguous())
+        torch.cuda.synchronize()
+        assert torch.equal(big, y)
+    finally:
+        dist.destroy_process_group()

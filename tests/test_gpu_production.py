@@ -367,3 +367,55 @@ def test_vit_base_b64_tie_resolved_end_to_end(dev):
     print(f"ViT-B b64 tie-resolved: rel {r['rel']:.2e}, {r['flips']} tie flips of {r['codes']} codes")
     assert not r["missing"] and not r["bad"], (r["missing"], r["bad"])
     assert r["rel"] <= TIE_E2E, r["rel"]
+
+
+# ---- configs[3]: ViT-L/16 @ 384, batch 128 (M = 128 * 577 = 73 856 token rows) ----------------------------------
+B128, TOK_L = 128, 577
+M128 = B128 * TOK_L           # 73 856
+
+
+@pytest.mark.parametrize("N,K,layer", [(4096, 1024, "fc1"), (1024, 4096, "fc2")])
+def test_gemm_vitl_b128_int32_exact(dev, N, K, layer):
+    """The ViT-L/16 @ 384 MLP GEMMs at the configs[3] bench size, int32-exact (VERDICT r03 #2)."""
+    assert _tiles(M128, N) > 2 * BLOCKS_PER_CU * _cus(dev), "must run several tiles per persistent block"
+    a, w, A, packed, npad, kpad = _gemm_case(dev, M128, N, K, seed=N + 2 * K)
+    C = torch.full((M128, N), -7, dtype=torch.int32, device=dev)
+    _lib.gemm(A, M128, kpad, packed, _lib.W4, N, npad, None, None, None, _lib.EPI_I32, C)
+    got = C.cpu()
+    del C, A
+    ref = _exact_accumulators(a, w)
+    bad = (got.float() != ref)
+    assert not bad.any(), f"{layer}: {int(bad.sum())} wrong accumulators, first at {bad.nonzero()[0].tolist()}"
+
+
+def test_qkv_split_attention_vitl_b128(dev):
+    """configs[3]'s attention at its bench size: the qkv GEMM into fp16 hi/lo head planes (qvit_gemm_qkv_split,
+    M = 73 856, N = 3 072, K = 1 024), then the streaming split attention (qvit_attention_split: B 128, H 16,
+    N 577, 128 x 16 x 10 (image, head, 64-query group) units over the persistent grid), against fp64 attention of
+    the planes' exact values on the images at both ends of every XCD's unit range (images 16 x and 16 x + 15)."""
+    B, N, H, K = B128, TOK_L, 16, 1024
+    C = 64 * H
+    ngroups = (N + 63) // 64
+    assert B * H * ngroups > 2 * 2 * _cus(dev), "each attention workgroup must walk several units"
+    g = torch.Generator().manual_seed(31)
+    a = torch.randint(-60, 61, (B * N, K), generator=g, dtype=torch.int16)
+    w = torch.randint(-7, 8, (3 * C, K), generator=g, dtype=torch.int16)
+    bias = torch.randn(3 * C, generator=g) * 0.3
+    packed, npad, kpad = pack_codes(w, _lib.W4, dev)
+    A = act_buffer(a, kpad, dev)
+    del a
+    hi = torch.empty(B * N * 3 * C, dtype=torch.float16, device=dev)
+    lo = torch.empty_like(hi)
+    _lib.gemm_qkv_split(A, B * N, kpad, packed, _lib.W4, 3 * C, npad, _p(0.004, dev), _p(0.003, dev),
+                        _lib.pad_bias(bias.to(dev), 3 * C, npad, dev), N, 1.0, hi, lo)
+    out = torch.full((B * N, C), float("nan"), device=dev)
+    _lib.attention_split(hi, lo, B, N, H, 64, 0.125, out, _lib.ATT_F32, 1.0)
+    torch.cuda.synchronize()
+    sel = [16 * x + e for x in range(8) for e in (0, 15)]
+    planes = (hi.view(B, 3 * H, N, 64)[sel].double() + lo.view(B, 3 * H, N, 64)[sel].double()).cpu()
+    q, k, v = planes[:, :H], planes[:, H:2 * H], planes[:, 2 * H:]
+    ref = (((q @ k.transpose(-2, -1)) * 0.125).softmax(dim=-1) @ v).transpose(1, 2).reshape(len(sel), N, C)
+    got = out.view(B, N, C)[sel].cpu().double()
+    assert torch.isfinite(got).all()
+    err = (got - ref).abs().max().item()
+    assert err <= 2e-6 * ref.abs().max().item(), err

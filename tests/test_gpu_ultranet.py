@@ -192,3 +192,39 @@ def test_int_deploy_argument_validation(dev):
     assert call(sb=0) == -1 and call(ob=8) == -1 and call(cin=24) == -1 and call(H=15) == -1
     assert call(inc=None) == -3 and call(inp=x.data_ptr() + 4) == -2
     torch.cuda.synchronize()
+
+
+# ---- production schedule (configs[4]: b256 @ 416) -------------------------------------------------------------
+def test_production_schedule_b256(dev):
+    """configs[4] at its bench size: batch 256 at 416 x 416, where every persistent conv workgroup walks tens of
+    tiles through the double-buffered tile stream. Layers 0 .. 2 run on all 256 images, each
+    stage-forced (layer k + 1 gets the device's layer-k codes), and are checked against the oracle's block on the
+    images at both ends of every XCD's contiguous tile range (images 32 x and 32 x + 31: each XCD owns 32 whole
+    images of every layer); then the fused forward end to end on those images."""
+    B, size = 256, 416
+    model = random_ultranet(seed=0, device=dev, calib_batch=2, img_size=size)
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    img = synthetic_images_u8(B, size, seed=21)
+    sel = [32 * x + e for x in range(8) for e in (0, 31)]
+    plan, _ = model._build_plan(dev)
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    # layer-0 tiles: 16 x 32 pre-pool pixels, at most 8 resident workgroups per CU
+    assert B * (size // 16) * (size // 32) > 2 * 8 * cus, "each workgroup must walk several tiles"
+    c0, a0, s0, _, _ = plan[0]
+    h = _lib.ultra_conv0(img.to(dev), c0, a0, s0, 4)
+    want = U.ultranet_block(sd, 0, img[sel])
+    assert_codes(h[sel], codes_of(want))
+    for k in (1, 2):
+        codes, alpha, shift, cout, pool = plan[k]
+        x_sel = h[sel].cpu().permute(0, 3, 1, 2).float() / 15.0        # the device's codes as the oracle's input
+        h = _lib.ultra_conv(h, 3, codes, cout, 4, 4, alpha, shift, _lib.ULTRA_CODES_POOL if pool else _lib.ULTRA_CODES)
+        assert_codes(h[sel], codes_of(U.ultranet_block(sd, k, x_sel)))
+    torch.cuda.synchronize()
+    del h
+    with torch.no_grad():
+        gio, gp = model(img.to(dev))
+        io, p = U.ultranet_forward(sd, img[sel])
+        io64, p64 = U.ultranet_forward({k: v.double() for k, v in sd.items()}, img[sel].double())
+    for got, want, want64 in ((gio[sel], io, io64), (gp[0][sel], p, p64)):
+        floor = rel(want64, want)
+        assert rel(got, want) <= max(1e-3, 2.5 * floor), (rel(got, want), floor)
