@@ -24,6 +24,9 @@
  *   qvit_gemm_wonly           quant_layers.py:495-499 in the default WEIGHT_ONLY mode (quant_model.py:23): fp32
  *                             activations x int4/int8 weight codes on bf16 MFMA (x split into three exact
  *                             bf16 terms), d_wt * acc + bias — F.linear(x, quantize_weight(W), b).
+ *   qvit_conv_wonly           quant_layers.py:575-587 (QuantizeConv2d.forward, WEIGHT_ONLY) and quant_ultra.py:85-89
+ *                             (Conv2d_Q.forward): the same contraction as an implicit GEMM over the NCHW input
+ *                             (patches gathered in the kernel), NCHW fp32 out — F.conv2d(x, quantize_weight(W), b).
  *   qvit_ultra_*              4-bit quantization/quant_ultra.py:8-91 + mymodel.py:62-144 (UltraNet: weight
  *                             codes, BN folding, fused conv+BN+quantizer+maxpool blocks, YOLO decode).
  *   qvit_attention            vit_model.py:133-149 (Attention.forward between qkv and proj):
@@ -211,6 +214,25 @@ int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda,
 int qvit_gemm_wonly(const float* X, int64_t M, int64_t K, int64_t ldx, const void* Wp, int wfmt,
                     int64_t N, int64_t npad, const float* d_wt, const float* bias, float* Y, int64_t ldy,
                     float* workspace, int64_t workspace_bytes, hipStream_t stream);
+
+/*
+ * Weight-only convolution (QuantizeConv2d.forward, quant_layers.py:575-587, quant_mode WEIGHT_ONLY; UltraNet's
+ * Conv2d_Q.forward, quant_ultra.py:85-89, whose quantize_fn values are k / (2^(w_bit-1) - 1)):
+ *   Y[b][n][oy][ox] = d_wt * sum_{c,ky,kx} X[b][c][oy sh - ph + ky dh][ox sw - pw + kx dw] k_w[n][(c kh + ky) kw + kx]
+ *                     + bias[n]   (zero padding; groups = 1)
+ *   X      : fp32 NCHW [B][C][H][W], contiguous (any alignment).
+ *   Wp     : qvit_pack_weight image of the codes [N][C kh kw] in the weight's flattening order (npad rows, kpad
+ *            == K >= C kh kw columns, K % QVIT_TILE_K == 0); wfmt as qvit_gemm_wonly.
+ *   d_wt, bias : as qvit_gemm_wonly.
+ *   Y      : fp32 NCHW [B][N][OH][OW] contiguous, OH = (H + 2 ph - dh (kh - 1) - 1) / sh + 1 (OW alike).
+ *   workspace : as qvit_gemm_wonly (split K for few output pixels).
+ * The patch rows are never materialised: the kernel gathers them from X stage by stage. Same arithmetic as
+ * qvit_gemm_wonly on the patch matrix.
+ */
+int qvit_conv_wonly(const float* X, int64_t B, int64_t C, int64_t H, int64_t W, int kh, int kw, int sh, int sw,
+                    int ph, int pw, int dh, int dw, const void* Wp, int wfmt, int64_t N, int64_t npad, int64_t K,
+                    const float* d_wt, const float* bias, float* Y, float* workspace, int64_t workspace_bytes,
+                    hipStream_t stream);
 
 /*
  * The residual contraction of a transformer block with the next LayerNorm behind it, in one launch:

@@ -66,6 +66,8 @@ _SIGNATURES = {
     "qvit_gemm": [_c_p, _i64, _i64, _i64, _c_p, _i32, _i64, _i64, _c_p, _c_p, _c_p, _i32, _c_p, _i64,
                   _i32, _c_p, _c_p, _c_p, _i32, _c_p, _c_p],
     "qvit_gemm_wonly": [_c_p, _i64, _i64, _i64, _c_p, _i32, _i64, _i64, _c_p, _c_p, _c_p, _i64, _c_p, _i64, _c_p],
+    "qvit_conv_wonly": [_c_p, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _c_p, _i32,
+                        _i64, _i64, _i64, _c_p, _c_p, _c_p, _c_p, _i64, _c_p],
     "qvit_epi_table_build": [_i32, _i32, _c_p, _c_p, _c_p, _i32, _f32, _f32, _i64, _c_p, _c_p],
     "qvit_gemm_resid_ln": [_c_p, _i64, _i64, _i64, _c_p, _i32, _i64, _i64, _c_p, _c_p, _c_p, _c_p, _i64, _c_p, _c_p,
                            _f32, _i32, _c_p, _c_p, _c_p, _i32, _c_p, _c_p, _i64, _i64, _c_p, _c_p],
@@ -300,6 +302,27 @@ def gemm_wonly(X: torch.Tensor, M: int, K: int, packed: torch.Tensor, wfmt: int,
                                   _ptr(bias_pad), _ptr(Y), Y.stride(0), _ptr(ws), 0 if ws is None else ws.numel() * 4,
                                   _stream(X.device)), "qvit_gemm_wonly")
     return Y
+
+
+def conv_wonly(x: torch.Tensor, kernel_size, stride, padding, dilation, packed: torch.Tensor, wfmt: int, N: int,
+               npad: int, kpad: int, d_wt: torch.Tensor, bias_pad: Optional[torch.Tensor]) -> torch.Tensor:
+    """F.conv2d(x, d_wt * codes, bias) (groups 1, zero padding) with fp32 NCHW x on qvit_conv_wonly: an implicit
+    GEMM against the packed codes ([N][C kh kw] in the weight's flattening order). Returns NCHW fp32."""
+    _require_gpu(x, "activations")
+    if x.dtype != torch.float32 or not x.is_contiguous():
+        x = x.float().contiguous()
+    B, C, H, W = x.shape
+    (kh, kw), (sh, sw), (ph, pw), (dh, dw) = kernel_size, stride, padding, dilation
+    OH = (H + 2 * ph - dh * (kh - 1) - 1) // sh + 1
+    OW = (W + 2 * pw - dw * (kw - 1) - 1) // sw + 1
+    y = torch.empty((B, N, OH, OW), dtype=torch.float32, device=x.device)
+    M = B * OH * OW
+    small = (npad // 256) * ((M + 63) // 64) < 128
+    ws = wonly_workspace(x.device, M, npad) if small else None
+    _check(load().qvit_conv_wonly(_ptr(x), B, C, H, W, kh, kw, sh, sw, ph, pw, dh, dw, _ptr(packed), wfmt, N, npad,
+                                  kpad, _ptr(d_wt), _ptr(bias_pad), _ptr(y), _ptr(ws),
+                                  0 if ws is None else ws.numel() * 4, _stream(x.device)), "qvit_conv_wonly")
+    return y
 
 
 def resid_ln_counters(device: torch.device, rows: int, npad: int) -> torch.Tensor:

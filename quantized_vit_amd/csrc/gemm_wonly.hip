@@ -24,6 +24,10 @@
 // 65536 a, 256 h and l are bf16 exactly, every product with an x term is exact in fp32, the digits' terms stay
 // within about |k| (balanced: no cancellation beyond a factor 2), and one accumulator takes them all (three
 // MFMAs per x term and digit).
+// Convolution (qvit_conv_wonly: weight-only QuantizeConv2d, UltraNet's Conv2d_Q): an implicit GEMM, the x row of
+// output pixel m = (b, oy, ox) being its input patch in the weight's flattening order k = (c kh + ky) kw + kx,
+// gathered from the NCHW input while the stage loads (zero outside the image and for k >= C kh kw), so no patch
+// matrix is ever written; the epilogue stores y straight into the NCHW output (plane n of image b).
 // Few tiles (small M, e.g. one image): the K stages are split over `splits` workgroups per tile, each writing
 // its raw fp32 partial to a workspace, and wonly_reduce_kernel sums the partials in split order (deterministic)
 // and applies d_w / s and the bias.
@@ -67,13 +71,17 @@ QVIT_DEV void bytes_bf16(uint32_t d, uint32_t& lo, uint32_t& hi, float mul) {
   lo = hi16(f0, f1);
   hi = hi16(f2, f3);
 }
+// convolution geometry (CONV kernels); L = OH OW output pixels per image, kreal = C kh kw
+struct WoConv {
+  int C, H, W, kh, kw, sh, sw, ph, pw, dh, dw, OW, L, kreal;
+};
 QVIT_DEV float trunc_bf16(float x) { return __uint_as_float(__float_as_uint(x) & 0xFFFF0000u); }
 
-template <int WFMT>
+template <int WFMT, bool CONV>
 __global__ __launch_bounds__(256, WoGeo<WFMT>::MINB) void gemm_wonly_kernel(
     const float* __restrict__ X, int M, int K, int64_t ldx, const int8_t* __restrict__ Wp, int N, int npad,
     const float* __restrict__ d_wt, const float* __restrict__ bias, float* __restrict__ Y, int64_t ldy, int splits,
-    float* __restrict__ part) {
+    float* __restrict__ part, const WoConv cg) {
   using G = WoGeo<WFMT>;
   __shared__ __attribute__((aligned(16))) int8_t smem[2 * G::STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -101,6 +109,15 @@ __global__ __launch_bounds__(256, WoGeo<WFMT>::MINB) void gemm_wonly_kernel(
   const int xr = tid >> 2, xq = tid & 3;
   const int xm = (m0 + xr < M) ? m0 + xr : M - 1;  // rows past M: a valid row, never stored
   const float* xsrc = X + (int64_t)xm * ldx + 16 * xq;
+  // CONV: this row's image and the input position of its patch's top-left tap
+  const float* img = X;
+  int iy0 = 0, ix0 = 0;
+  if (CONV) {
+    const int b = xm / cg.L, p = xm - b * cg.L, oy = p / cg.OW;
+    img = X + (int64_t)b * cg.C * cg.H * cg.W;
+    iy0 = oy * cg.sh - cg.ph;
+    ix0 = (p - oy * cg.OW) * cg.sw - cg.pw;
+  }
   // (W16 / W24: piece i from digit image i / WPP, each image npad K bytes)
   constexpr int WPP = G::WPER / G::PARTS;
   const int8_t* wsrc = Wp + (int64_t)tn * nk * G::WBYTES + tid * 16 * WPP;
@@ -108,8 +125,28 @@ __global__ __launch_bounds__(256, WoGeo<WFMT>::MINB) void gemm_wonly_kernel(
   f4 xv[4];
   v4i wv[G::WPER];
   auto load = [&](int kt) __attribute__((always_inline)) {
+    if (CONV) {  // the 16 taps k0 .. k0 + 15 of the patch, (c, ky, kx) stepped along
+      const int k0 = kt * WO_BK + 16 * xq, khw = cg.kh * cg.kw;
+      int c = k0 / khw, r = k0 - c * khw, ky = r / cg.kw, kx = r - ky * cg.kw;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) xv[i] = *reinterpret_cast<const f4*>(xsrc + kt * WO_BK + 4 * i);
+      for (int i = 0; i < 16; ++i) {
+        const int iy = iy0 + ky * cg.dh, ix = ix0 + kx * cg.dw;
+        float v = 0.f;
+        if (k0 + i < cg.kreal && (unsigned)iy < (unsigned)cg.H && (unsigned)ix < (unsigned)cg.W)
+          v = img[((int64_t)c * cg.H + iy) * cg.W + ix];
+        xv[i >> 2][i & 3] = v;
+        if (++kx == cg.kw) {
+          kx = 0;
+          if (++ky == cg.kh) {
+            ky = 0;
+            ++c;
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) xv[i] = *reinterpret_cast<const f4*>(xsrc + kt * WO_BK + 4 * i);
+    }
 #pragma unroll
     for (int i = 0; i < G::WPER; ++i)
       wv[i] = *reinterpret_cast<const v4i*>(wsrc + (i / WPP) * wpart + (int64_t)kt * G::WBYTES + 16 * (i % WPP));
@@ -227,6 +264,18 @@ __global__ __launch_bounds__(256, WoGeo<WFMT>::MINB) void gemm_wonly_kernel(
   for (int s = 0; s < 4; ++s) {
     const int m = m0 + 16 * s + fr;
     if (m >= M) continue;
+    if (CONV) {  // NCHW: y[b][n][p], 16 lanes of a row group storing consecutive pixels of one plane
+      const int b = m / cg.L;
+      float* yp = Y + ((int64_t)b * N * cg.L + (m - b * cg.L));
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = nb + 4 * r + j;
+          if (n < N) yp[(int64_t)n * cg.L] = fmaf(alpha, acc[r][s][j], bcol[4 * r + j]);
+        }
+      continue;
+    }
     float* yr = Y + (int64_t)m * ldy + nb;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -250,7 +299,7 @@ template <int WFMT>
 __global__ __launch_bounds__(256) void wonly_reduce_kernel(const float* __restrict__ part, int splits, int M, int N,
                                                             int npad, const float* __restrict__ d_wt,
                                                             const float* __restrict__ bias, float* __restrict__ Y,
-                                                            int64_t ldy) {
+                                                            int64_t ldy, int L) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // one 4-column group per thread
   const int gpr = npad / 4;
   if (i >= (int64_t)M * gpr) return;
@@ -259,10 +308,57 @@ __global__ __launch_bounds__(256) void wonly_reduce_kernel(const float* __restri
   f4 a = *reinterpret_cast<const f4*>(part + (int64_t)m * npad + n);
   for (int sp = 1; sp < splits; ++sp) a += *reinterpret_cast<const f4*>(part + ((int64_t)sp * M + m) * npad + n);
   const float alpha = (*d_wt) * (WFMT == QVIT_W4 ? 0.0625f : 1.f);
+  if (L > 0) {  // NCHW output of a convolution (L pixels per plane)
+    const int b = m / L;
+    float* yp = Y + ((int64_t)b * N * L + (m - b * L));
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (n + j < N) yp[(int64_t)(n + j) * L] = fmaf(alpha, a[j], bias ? bias[n + j] : 0.f);
+    return;
+  }
   float* yr = Y + (int64_t)m * ldy + n;
 #pragma unroll
   for (int j = 0; j < 4; ++j)
     if (n + j < N) yr[j] = fmaf(alpha, a[j], bias ? bias[n + j] : 0.f);
+}
+
+// shared launch of the GEMM (CONV = false) and the implicit-GEMM convolution (CONV = true); arguments checked
+template <bool CONV>
+int wonly_launch(const float* X, int64_t M, int64_t K, int64_t ldx, const void* Wp, int wfmt, int64_t N, int64_t npad,
+                 const float* d_wt, const float* bias, float* Y, int64_t ldy, float* workspace, int64_t workspace_bytes,
+                 const WoConv& cg, hipStream_t stream) {
+  const int64_t ntiles = (npad / WO_BN) * ((M + WO_BM - 1) / WO_BM);
+  if (ntiles > INT32_MAX / 2) return QVIT_EINVAL;
+  // fewer tiles than half the CUs: split the K stages so that about 256 workgroups run (when the workspace
+  // holds the partials)
+  const int64_t nk = K / WO_BK;
+  int64_t splits = 1;
+  if (ntiles < 128 && nk >= 2 && workspace && !(((uintptr_t)workspace) & 15)) {
+    splits = std::min<int64_t>(nk, (256 + ntiles - 1) / ntiles);
+    while (splits > 1 && splits * M * npad * 4 > workspace_bytes) --splits;
+  }
+  const int64_t grid = splits > 1 ? ntiles * splits : (ntiles + 7) / 8 * 8;
+  const int8_t* w = reinterpret_cast<const int8_t*>(Wp);
+#define QVIT_WO_LAUNCH(F)                                                                                    \
+  hipLaunchKernelGGL((gemm_wonly_kernel<F, CONV>), dim3((unsigned)grid), dim3(256), 0, stream, X, (int)M, (int)K,  \
+                     ldx, w, (int)N, (int)npad, d_wt, bias, Y, ldy, (int)splits, workspace, cg)
+  if (wfmt == QVIT_W4) QVIT_WO_LAUNCH(QVIT_W4);
+  else if (wfmt == QVIT_W8) QVIT_WO_LAUNCH(QVIT_W8);
+  else if (wfmt == QVIT_W16) QVIT_WO_LAUNCH(QVIT_W16);
+  else QVIT_WO_LAUNCH(QVIT_W24);
+#undef QVIT_WO_LAUNCH
+  if (splits > 1) {
+    const int64_t groups = M * (npad / 4);
+    const unsigned rg = (unsigned)((groups + 255) / 256);
+    const int L = CONV ? cg.L : 0;
+    if (wfmt == QVIT_W4)
+      hipLaunchKernelGGL(wonly_reduce_kernel<QVIT_W4>, dim3(rg), dim3(256), 0, stream, workspace, (int)splits, (int)M,
+                         (int)N, (int)npad, d_wt, bias, Y, ldy, L);
+    else  // (W8 / W16 / W24 accumulators are unscaled)
+      hipLaunchKernelGGL(wonly_reduce_kernel<QVIT_W8>, dim3(rg), dim3(256), 0, stream, workspace, (int)splits, (int)M,
+                         (int)N, (int)npad, d_wt, bias, Y, ldy, L);
+  }
+  return qvit_hip_status(hipGetLastError());
 }
 
 }  // namespace
@@ -278,35 +374,31 @@ extern "C" int qvit_gemm_wonly(const float* X, int64_t M, int64_t K, int64_t ldx
   if ((ldx % 4) || (((uintptr_t)X) & 15) || (((uintptr_t)Wp) & 15)) return QVIT_EALIGN;
   if ((ldy % 4) || (((uintptr_t)Y) & 15) || (bias && (((uintptr_t)bias) & 15))) return QVIT_EALIGN;
   if (M == 0) return QVIT_OK;
-  const int64_t ntiles = (npad / WO_BN) * ((M + WO_BM - 1) / WO_BM);
-  if (ntiles > INT32_MAX / 2) return QVIT_EINVAL;
-  // fewer tiles than half the CUs: split the K stages so that about 256 workgroups run (when the workspace
-  // holds the partials)
-  const int64_t nk = K / WO_BK;
-  int64_t splits = 1;
-  if (ntiles < 128 && nk >= 2 && workspace && !(((uintptr_t)workspace) & 15)) {
-    splits = std::min<int64_t>(nk, (256 + ntiles - 1) / ntiles);
-    while (splits > 1 && splits * M * npad * 4 > workspace_bytes) --splits;
-  }
-  const int64_t grid = splits > 1 ? ntiles * splits : (ntiles + 7) / 8 * 8;
-  const int8_t* w = reinterpret_cast<const int8_t*>(Wp);
-#define QVIT_WO_LAUNCH(F)                                                                                    \
-  hipLaunchKernelGGL(gemm_wonly_kernel<F>, dim3((unsigned)grid), dim3(256), 0, stream, X, (int)M, (int)K, ldx, w, \
-                     (int)N, (int)npad, d_wt, bias, Y, ldy, (int)splits, workspace)
-  if (wfmt == QVIT_W4) QVIT_WO_LAUNCH(QVIT_W4);
-  else if (wfmt == QVIT_W8) QVIT_WO_LAUNCH(QVIT_W8);
-  else if (wfmt == QVIT_W16) QVIT_WO_LAUNCH(QVIT_W16);
-  else QVIT_WO_LAUNCH(QVIT_W24);
-#undef QVIT_WO_LAUNCH
-  if (splits > 1) {
-    const int64_t groups = M * (npad / 4);
-    const unsigned rg = (unsigned)((groups + 255) / 256);
-    if (wfmt == QVIT_W4)
-      hipLaunchKernelGGL(wonly_reduce_kernel<QVIT_W4>, dim3(rg), dim3(256), 0, stream, workspace, (int)splits, (int)M,
-                         (int)N, (int)npad, d_wt, bias, Y, ldy);
-    else  // (W8 / W16 / W24 accumulators are unscaled)
-      hipLaunchKernelGGL(wonly_reduce_kernel<QVIT_W8>, dim3(rg), dim3(256), 0, stream, workspace, (int)splits, (int)M,
-                         (int)N, (int)npad, d_wt, bias, Y, ldy);
-  }
-  return qvit_hip_status(hipGetLastError());
+  return wonly_launch<false>(X, M, K, ldx, Wp, wfmt, N, npad, d_wt, bias, Y, ldy, workspace, workspace_bytes,
+                             WoConv{}, stream);
+}
+
+extern "C" int qvit_conv_wonly(const float* X, int64_t B, int64_t C, int64_t H, int64_t W, int kh, int kw, int sh,
+                               int sw, int ph, int pw, int dh, int dw, const void* Wp, int wfmt, int64_t N,
+                               int64_t npad, int64_t K, const float* d_wt, const float* bias, float* Y,
+                               float* workspace, int64_t workspace_bytes, hipStream_t stream) {
+  if (!X || !Wp || !Y || !d_wt) return QVIT_ENULL;
+  if (wfmt != QVIT_W4 && wfmt != QVIT_W8 && wfmt != QVIT_W16 && wfmt != QVIT_W24) return QVIT_EINVAL;
+  if (B < 0 || C <= 0 || H <= 0 || W <= 0 || kh <= 0 || kw <= 0 || sh <= 0 || sw <= 0 || ph < 0 || pw < 0 ||
+      dh <= 0 || dw <= 0)
+    return QVIT_EINVAL;
+  if (C > INT32_MAX || H > INT32_MAX || W > INT32_MAX || B * C * H * W > (int64_t)1 << 40) return QVIT_EINVAL;
+  const int64_t OH = (H + 2 * ph - (int64_t)dh * (kh - 1) - 1) / sh + 1;
+  const int64_t OW = (W + 2 * pw - (int64_t)dw * (kw - 1) - 1) / sw + 1;
+  const int64_t kreal = C * kh * kw;
+  if (H + 2 * ph < (int64_t)dh * (kh - 1) + 1 || W + 2 * pw < (int64_t)dw * (kw - 1) + 1) return QVIT_EINVAL;
+  if (K <= 0 || K % QVIT_TILE_K || K < kreal || K > (1 << 24) || N <= 0 || npad < N || npad % WO_BN ||
+      npad > INT32_MAX / 2)
+    return QVIT_EINVAL;
+  const int64_t M = B * OH * OW;
+  if (M > INT32_MAX / 2 || OH * OW > INT32_MAX / 2) return QVIT_EINVAL;
+  if ((((uintptr_t)Wp) & 15) || (bias && (((uintptr_t)bias) & 15))) return QVIT_EALIGN;
+  if (M == 0) return QVIT_OK;
+  const WoConv cg{(int)C, (int)H, (int)W, kh, kw, sh, sw, ph, pw, dh, dw, (int)OW, (int)(OH * OW), (int)kreal};
+  return wonly_launch<true>(X, M, K, K, Wp, wfmt, N, npad, d_wt, bias, Y, N, workspace, workspace_bytes, cg, stream);
 }

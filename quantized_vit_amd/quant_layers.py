@@ -436,7 +436,6 @@ class QuantizeMixin:
 
 
 _GELU_MAX_SLOPE = 1.1289   # max of d/dv [v Phi(v)] (at v ~ 1.41)
-WONLY_CONV_BYTES = 1 << 30  # patch-row bytes per chunk of a weight-only QuantizeConv2d
 
 
 def _gelu(v: float) -> float:
@@ -628,25 +627,10 @@ class QuantizeConv2d(nn.Conv2d, QuantizeMixin):
         x = self.quantize_act(input_.float()) if self.quant_mode == QuantizationMode.WEIGHT_AND_ACTIVATION \
             else input_.float()
         if plan.extra.get("wonly") and self._int_conv_ok():
-            # weight-only / wide levels: the input patches (K order (c, kh, kw) = the weight flattening) as fp32
-            # rows against the packed codes (qvit_gemm_wonly)
-            B = x.shape[0]
-            OH = (x.shape[2] + 2 * self.padding[0] - self.dilation[0] * (self.kernel_size[0] - 1) - 1) // self.stride[0] + 1
-            OW = (x.shape[3] + 2 * self.padding[1] - self.dilation[1] * (self.kernel_size[1] - 1) - 1) // self.stride[1] + 1
-            L = OH * OW
-            # images in chunks whose patch rows stay within a byte budget (a 3x3 conv at 416 x 416 and B = 256
-            # would otherwise materialise ~22 GB of zero-padded fp32 rows)
-            per_img = L * plan.kpad * 4 * 2
-            step = max(1, min(B, WONLY_CONV_BYTES // max(per_img, 1)))
-            y = torch.empty((B, L, plan.n), dtype=torch.float32, device=x.device)
-            for b0 in range(0, B, step):
-                xb = x.detach()[b0:b0 + step]
-                cols = F.unfold(xb, self.kernel_size, self.dilation, self.padding, self.stride)  # [b, K, L]
-                x2 = torch.zeros((xb.shape[0] * L, plan.kpad), dtype=torch.float32, device=x.device)
-                x2.view(xb.shape[0], L, plan.kpad)[:, :, :plan.k] = cols.transpose(1, 2)
-                del cols
-                y[b0:b0 + step] = self._wonly_rows(x2, plan).view(xb.shape[0], L, plan.n)
-            return y.view(B, OH, OW, plan.n).permute(0, 3, 1, 2).contiguous()
+            # weight-only / wide levels: an implicit GEMM of the NCHW input against the packed codes
+            # (qvit_conv_wonly: patches gathered in the kernel, NCHW out)
+            return _lib.conv_wonly(x.detach(), self.kernel_size, self.stride, self.padding, self.dilation,
+                                   plan.packed, plan.wfmt, plan.n, plan.npad, plan.kpad, plan.d_wt, plan.bias_pad)
         w = self.w_fakequant(plan).view_as(self.weight)
         return F.conv2d(x.detach(), w, None if self.bias is None else self.bias.detach(), self.stride,
                         self.padding, self.dilation, self.groups)

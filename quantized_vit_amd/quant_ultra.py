@@ -4,8 +4,14 @@ UltraNet): same factory / class names and forward semantics, computed on the ROC
   uniform_quantize(k)        quant_ultra.py:8-27   round(x * (2^k - 1)) / (2^k - 1)  (k = 1: sign, 32: identity)
   weight_quantize_fn(w_bit)  :30-56   tanh -> / max|tanh| -> (w_bit-1)-bit uniform quantizer (HIP codes)
   activation_quantize_fn     :59-73   clamp(x, 0, 1) -> a_bit uniform quantizer (HIP)
-  conv2d_Q_fn(w_bit)         :76-91   Conv2d_Q: conv with quantized weights
-  batchNorm2d_Q_fn / batchNorm1d_Q_fn / linear_Q_fn  :94-222 (not used by UltraNetQua; kept for API parity)
+  conv2d_Q_fn(w_bit)         :76-91   Conv2d_Q: conv with quantized weights -- qvit_conv_wonly (implicit GEMM of the
+                                      fp32 input against the int weight codes, d_w = 1/(2^(w_bit-1)-1))
+  linear_Q_fn(w_bit)         :210-222 Linear_Q -- qvit_gemm_wonly on the same codes
+  batchNorm2d_Q_fn / batchNorm1d_Q_fn  :94-207 (not used by UltraNetQua; kept for API parity)
+
+Conv2d_Q / Linear_Q with 2 <= w_bit <= 8 (UltraNet: 4) run on the hand-written kernels; their weight codes are
+packed once per weight version. w_bit 32 (no quantization: a plain conv / linear) and w_bit 1 (the reference's
+k = 0 quantizer divides by zero) keep the library call on the device, as do grouped or non-zero-padded convs.
 
 The network-level fused path (conv + BN + quantizer + max pool on codes) is in ultranet.py; these
 modules are the per-layer surface. Forward-only (inference): the reference's straight-through
@@ -93,6 +99,41 @@ class activation_quantize_fn(nn.Module):
         return _lib.fake_quant_f32(x, _lib.QT_ULTRA_ACT, None, None, None, 2 ** self.a_bit - 1).reshape(x.shape)
 
 
+class _PackedCodes:
+    """Packed weight codes of weight_quantize_fn for qvit_gemm_wonly / qvit_conv_wonly: the HIP quantizer's codes
+    k (values k / n, n = 2^(w_bit-1) - 1) re-ordered to the weight's flattening (c, kh, kw), packed int4 (n <= 7)
+    or int8, with d_w = 1/n. Rebuilt when the weight or bias changes (in place or replaced)."""
+
+    def __init__(self):
+        self.key = None
+
+    def get(self, weight: torch.Tensor, bias, w_bit: int):
+        key = (weight.data_ptr(), weight._version, tuple(weight.shape), weight.device,
+               None if bias is None else (bias.data_ptr(), bias._version))
+        if key == self.key:
+            return self
+        w4 = weight.detach() if weight.dim() == 4 else weight.detach().reshape(weight.shape[0], -1, 1, 1)
+        cout, cin, kh, kw = w4.shape
+        k = cin * kh * kw
+        self.n, self.npad, self.kpad = cout, _round_up(cout, _lib.TILE_N), _round_up(k, _lib.TILE_K)
+        codes = _lib.ultra_weight_codes(w4, w_bit, _round_up(k, 16), cout)       # (ky, kx, c) order
+        codes = codes[:, :k].view(cout, kh, kw, cin).permute(0, 3, 1, 2).reshape(cout, k).float().contiguous()
+        n_lvl = 2 ** (w_bit - 1) - 1
+        dev = weight.device
+        self.wfmt = _lib.W4 if n_lvl <= 7 else _lib.W8
+        ovf = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.packed = _lib.pack_weight(codes, _lib.QT_LINEAR, torch.ones(1, device=dev),
+                                       torch.full((1,), 1024.0, device=dev), None, self.wfmt, self.npad, self.kpad, ovf)
+        self.d_wt = torch.full((1,), 1.0 / n_lvl, dtype=torch.float32, device=dev)
+        self.bias_pad = _lib.pad_bias(bias, cout, self.npad, dev)
+        self.key = key
+        return self
+
+
+def _codes_path(w_bit: int) -> bool:
+    return 2 <= w_bit <= 8
+
+
 def conv2d_Q_fn(w_bit):
     """quant_ultra.py:76-91."""
 
@@ -102,8 +143,16 @@ def conv2d_Q_fn(w_bit):
             super().__init__(in_channels, out_channels, kernel_size, stride, padding, dilation, groups, bias)
             self.w_bit = w_bit
             self.quantize_fn = weight_quantize_fn(w_bit=w_bit)
+            self._codes = _PackedCodes()
 
         def forward(self, input, order=None):
+            if _codes_path(self.w_bit):
+                _check_gpu(input, "input")
+            if _codes_path(self.w_bit) and self.groups == 1 and self.padding_mode == "zeros" and \
+                    not isinstance(self.padding, str) and input.dim() == 4:
+                c = self._codes.get(self.weight, self.bias, self.w_bit)
+                return _lib.conv_wonly(input.detach(), self.kernel_size, self.stride, self.padding, self.dilation,
+                                       c.packed, c.wfmt, c.n, c.npad, c.kpad, c.d_wt, c.bias_pad)
             weight_q = self.quantize_fn(self.weight)
             return F.conv2d(input, weight_q, self.bias, self.stride, self.padding, self.dilation, self.groups)
 
@@ -161,8 +210,23 @@ def linear_Q_fn(w_bit):
             super().__init__(in_features, out_features, bias)
             self.w_bit = w_bit
             self.quantize_fn = weight_quantize_fn(w_bit=w_bit)
+            self._codes = _PackedCodes()
 
         def forward(self, input):
-            return F.linear(input, self.quantize_fn(self.weight), self.bias)
+            if not _codes_path(self.w_bit):
+                return F.linear(input, self.quantize_fn(self.weight), self.bias)
+            _check_gpu(input, "input")
+            c = self._codes.get(self.weight, self.bias, self.w_bit)
+            x2 = input.detach().reshape(-1, self.in_features)
+            if (x2.dtype != torch.float32 or x2.stride(-1) != 1 or c.kpad != self.in_features or x2.stride(0) % 4
+                    or x2.data_ptr() % 16):
+                xp = torch.zeros((x2.shape[0], c.kpad), dtype=torch.float32, device=x2.device)
+                xp[:, :self.in_features] = x2
+                x2 = xp
+            ldy = _round_up(c.n, 4)
+            y = torch.empty((x2.shape[0], ldy), dtype=torch.float32, device=x2.device)
+            _lib.gemm_wonly(x2, x2.shape[0], c.kpad, c.packed, c.wfmt, c.n, c.npad, c.d_wt, c.bias_pad, y)
+            y = y if ldy == c.n else y[:, :c.n]
+            return y.reshape(*input.shape[:-1], c.n)
 
     return Linear_Q

@@ -180,9 +180,20 @@ class UltraNetQua(nn.Module):
     def forward(self, x):
         if self.fused_ok(x):
             return self.forward_fused(x)
+        return self.forward_modules(x)
+
+    def forward_modules(self, x):
+        """mymodel.py:134-144 module by module: Conv2d_Q on qvit_conv_wonly, activation_quantize_fn on the HIP
+        quantizer; BatchNorm2d and MaxPool2d on ATen's own kernels (the MIOpen batch-norm route off, so no
+        library kernel is on the path). Any image size, training mode included."""
         img_size = x.shape[-2:]
         yolo_out = []
-        x = self.layers(x)
+        prev = torch.backends.cudnn.enabled
+        torch.backends.cudnn.enabled = False
+        try:
+            x = self.layers(x)
+        finally:
+            torch.backends.cudnn.enabled = prev
         x = self.yololayer(x, img_size)
         yolo_out.append(x)
         if self.training:
