@@ -143,6 +143,7 @@ QVIT_DEV _Float16 lo_h(float x) { return (_Float16)(x - (float)(_Float16)x); }  
 // LDS (23 KiB per workgroup) rather than registers bounds residency at 7 workgroups per CU; 4 patches per group
 // at 4 workgroups per CU (round-3 build): 344-353 us vs 283-286 us at b256 (profiles/r03_conv0_occupancy_ab.txt)
 constexpr int C0_G = 1;     // patches per MFMA group
+constexpr int C0_WAVE_OUT = 2 * (C0_TX / 2) * C0_OUT;  // a wave's pooled codes per tile: 512 B
 constexpr int C0_OCC = 6;   // workgroups per CU
 template <bool VEC>
 __global__ __launch_bounds__(256, C0_OCC) void ultra_conv0_mfma_kernel(const float* __restrict__ img, int B, int H, int W,
@@ -151,12 +152,15 @@ __global__ __launch_bounds__(256, C0_OCC) void ultra_conv0_mfma_kernel(const flo
                                                                const float* __restrict__ shift, float levels,
                                                                int8_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) int8_t smem[2][2 * C0_PLANE];
+  __shared__ __attribute__((aligned(16))) int8_t codes_l[4][C0_WAVE_OUT];  // each wave's pooled codes of a tile
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int n = lane & 15, g = lane >> 4;
   // A row n = pixel (2 ((n >> 2) >> 1) + ((n & 3) >> 1), 2 ((n >> 2) & 1) + (n & 1)) of the 4x4 patch
   const int py = 2 * (n >> 3) + ((n >> 1) & 1), px = 2 * ((n >> 2) & 1) + (n & 1);
   const int Ho = H / 2, Wo = W / 2;
+  // this lane's code byte of patch pq: pooled row g >> 1, pooled column 2 pq + (g & 1), channel n
+  int8_t* cw = codes_l[wave] + ((g >> 1) * (C0_TX / 2) + (g & 1)) * C0_OUT + n;
 
   // B operands: weights [o = n][c][ky][kx] split hi / lo in the K order above; record r (0, 1) of group g is tap
   // (ky, kx) = g < 3 ? (g, r) : (r, 2)
@@ -173,16 +177,28 @@ __global__ __launch_bounds__(256, C0_OCC) void ultra_conv0_mfma_kernel(const flo
   }
   const float al = alpha[n], sh = shift[n];
   const bool up = !(al < 0.f);  // BN increasing in the accumulator
+  // both BN constants arrive here, before the loop: a use inside the loop would otherwise carry a vmcnt(0) that
+  // also drains the next tile's halo prefetch at the first patch
+  asm volatile("" ::"v"(al), "v"(sh));
 
   const int tiles_y = (H + C0_TY - 1) / C0_TY, tiles_x = (W + C0_TX - 1) / C0_TX;
   const int ntiles = B * tiles_y * tiles_x;
   const int64_t HW = (int64_t)H * W;
+  // tile t = (b tiles_y + ty) tiles_x + tx as (b, ty, tx); the walk advances t by a fixed team, so the
+  // coordinates advance by the team's own with carries (no division per tile)
+  struct TPos {
+    int b, ty, tx;
+  };
+  auto tpos = [&](int t) __attribute__((always_inline)) {
+    const int row = t / tiles_x;
+    return TPos{row / tiles_y, row - (row / tiles_y) * tiles_y, t - row * tiles_x};
+  };
   // this thread's halo quad (hy, 4 qx .. 4 qx + 3) of tile t -> registers (zero outside the image)
   const int qy = tid / (C0_HX / 4), qx = tid - qy * (C0_HX / 4);
   c0f4 xin[3];
-  auto load_tile = [&](int t) __attribute__((always_inline)) {
+  auto load_tile = [&](const TPos& p) __attribute__((always_inline)) {
     if (tid >= C0_QUADS) return;
-    const int tx0 = (t % tiles_x) * C0_TX, ty0 = ((t / tiles_x) % tiles_y) * C0_TY, b = t / (tiles_x * tiles_y);
+    const int b = p.b, ty0 = p.ty * C0_TY, tx0 = p.tx * C0_TX;
     const float* base = img + (int64_t)b * 3 * HW;
     const int y = ty0 - 1 + qy, x = tx0 - 4 + 4 * qx;
     const bool row = y >= 0 && y < H;
@@ -225,15 +241,41 @@ __global__ __launch_bounds__(256, C0_OCC) void ultra_conv0_mfma_kernel(const flo
   const TileWalk tw = tile_walk(ntiles);
   int t = tw.lo + tw.slot;
   if (t >= tw.hi) return;
-  load_tile(t);
+  TPos cur = tpos(t);
+  const TPos step = tpos(tw.team);
+  auto advance = [&](TPos p) __attribute__((always_inline)) {
+    p.tx += step.tx;
+    if (p.tx >= tiles_x) p.tx -= tiles_x, p.ty += 1;
+    p.ty += step.ty;
+    if (p.ty >= tiles_y) p.ty -= tiles_y, p.b += 1;
+    p.b += step.b;
+    return p;
+  };
+  load_tile(cur);
   stage_tile(smem[0]);
   __syncthreads();
+  // the wave's pooled codes of a tile (2 rows x 16 columns x 16 channels) leave as 16-B pixels, 16 lanes per
+  // 256-B output row; the wave reads back only what it wrote (its LDS operations complete in order). Issued
+  // after the next tile's halo loads: a store ahead of them would make their issue wait for its completion.
+  auto flush = [&](int b, int ty0, int tx0) __attribute__((always_inline)) {
+    __builtin_amdgcn_wave_barrier();
+    if (lane < 32) {
+      const int yo = ((ty0 + 4 * wave) >> 1) + (lane >> 4), xo = (tx0 >> 1) + (lane & 15);
+      const uint4 v = *reinterpret_cast<const uint4*>(codes_l[wave] + lane * C0_OUT);
+      if (yo < Ho && xo < Wo) *reinterpret_cast<uint4*>(out + (((int64_t)b * Ho + yo) * Wo + xo) * C0_OUT) = v;
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
+  int pb = 0, pty = 0, ptx = 0;  // the previous tile, its codes still in codes_l
   for (int it = 0; t < tw.hi; t += tw.team, ++it) {
     const int8_t* buf = smem[it & 1];
     const int tn = t + tw.team;
-    if (tn < tw.hi) load_tile(tn);  // lands while this tile computes
-    const int tx0 = (t % tiles_x) * C0_TX, ty0 = ((t / tiles_x) % tiles_y) * C0_TY, b = t / (tiles_x * tiles_y);
-    const int yo = ((ty0 + 4 * wave) >> 1) + (g >> 1);  // this lane's pool window
+    const TPos nxt = advance(cur);
+    if (tn < tw.hi) load_tile(nxt);  // lands while this tile computes
+    if (it > 0) flush(pb, pty, ptx);
+    const int b = cur.b, ty0 = cur.ty * C0_TY, tx0 = cur.tx * C0_TX;
+    pb = b, pty = ty0, ptx = tx0;
+    cur = nxt;
     // A fragment records (halo pixel of tap (ky, kx): row 4 wave + py + ky, column px + kx + 3, + 4 per patch):
     // chunk 0 records r0, r1 of group g; chunk 1 = tap (2, 2) hi, then its lo (g = 0) or hi again
     auto rec = [&](int ky, int kx) { return buf + ((4 * wave + py + ky) * C0_HX + px + kx + 3) * 8; };
@@ -274,15 +316,15 @@ __global__ __launch_bounds__(256, C0_OCC) void ultra_conv0_mfma_kernel(const flo
         const float mn = fmin_nn(fmin_nn(acc[q][0], acc[q][1]), fmin_nn(acc[q][2], acc[q][3]));
         const float y = __fadd_rn(__fmul_rn(up ? mx : mn, al), sh);
         const int code = (int)rintf(__builtin_amdgcn_fmed3f(y, 0.f, 1.f) * levels);
-        const int xo = ((tx0 + 4 * (pq + q)) >> 1) + (g & 1);
-        const uint32_t word = pack_quad(code);
-        if ((n & 3) == 0 && yo < Ho && xo < Wo)
-          *reinterpret_cast<uint32_t*>(out + (((int64_t)b * Ho + yo) * Wo + xo) * C0_OUT + n) = word;
+        cw[2 * (pq + q) * C0_OUT] = (int8_t)code;
       }
+      // one patch at a time (without the fence the scheduler hoists later patches' fragment reads: spills)
+      __builtin_amdgcn_sched_barrier(0);
     }
     if (tn < tw.hi) stage_tile(smem[(it + 1) & 1]);  // the other buffer: its last reader finished a barrier ago
     __syncthreads();
   }
+  flush(pb, pty, ptx);
 }
 
 // ---- integer deploy (quantization.py:24-31,68-89; ultranet_param_gen.py) --------------------------------
