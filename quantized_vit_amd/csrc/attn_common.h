@@ -100,7 +100,7 @@ QVIT_DEV void attend(int nt, bool mask, const int8_t* st, const h8 (&qh)[T][2], 
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
         s[i][kt] = f4{0.f, 0.f, 0.f, 0.f};
-        if (i == NT - 1 && nt < NT) continue;  // wave-uniform: no 4th tile
+        if (i >= nt) continue;                 // wave-uniform: the wave has nt tiles
         if (kt == 1 && half) continue;        // wave-uniform
 #pragma unroll
         for (int c = 0; c < 2; ++c) s[i][kt] = mfma3(kh[kt][c], kl[kt][c], qh[i][c], ql[i][c], s[i][kt]);
@@ -121,7 +121,7 @@ QVIT_DEV void attend(int nt, bool mask, const int8_t* st, const h8 (&qh)[T][2], 
   h8 ph[NT], pl[NT];
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
-    if (i == NT - 1 && nt < NT) continue;
+    if (i >= nt) continue;
     float x[8];
     // raw scores of this lane's query; sl2 (> 0) goes into the exponent's fma: the max of the scaled
     // scores is sl2 times the max of the raw ones (rounding is monotone)
@@ -163,8 +163,8 @@ QVIT_DEV void attend(int nt, bool mask, const int8_t* st, const h8 (&qh)[T][2], 
       vl[dt] = join(tr_read(st + 3 * IMGS, voffs[dt]), tr_read(st + 3 * IMGS, voffs[dt] + 16 * 128));
     }
 #pragma unroll
-    for (int i = 0; i < NT - 1; ++i) o[i][dt] = mfma3(vh[dt], vl[dt], ph[i], pl[i], o[i][dt]);
-    if (nt == NT) o[NT - 1][dt] = mfma3(vh[dt], vl[dt], ph[NT - 1], pl[NT - 1], o[NT - 1][dt]);
+    for (int i = 0; i < NT; ++i)
+      if (i < nt) o[i][dt] = mfma3(vh[dt], vl[dt], ph[i], pl[i], o[i][dt]);
   }
   sp.mark(3);
 }
