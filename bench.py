@@ -415,6 +415,9 @@ def main():
             k["frac_hbm_peak"] = k["hbm_GBs_algorithmic"] / HBM_PEAK_GBS
         if pmc and n in pmc.get("kernels", {}):
             k["pmc"] = pmc["kernels"][n]
+            tb = k["pmc"].get("traffic_bytes")
+            if tb:   # HBM bytes per launch (PMC) over the algorithmic bytes: re-reads show up as > 1
+                k["traffic_over_algorithmic"] = tb / w["bytes"]
         kernels[n] = k
     total_ops = model_gemm_ops(model, B)
 

@@ -353,11 +353,13 @@ __global__ __launch_bounds__(256, 4) void ultra_conv0_int_mfma_kernel(const uint
                                                                    const int* __restrict__ bias, int sbits,
                                                                    int levels, int8_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) int8_t smem[2][C0I_PLANE];
+  __shared__ __attribute__((aligned(16))) int8_t codes_l[4][C0_WAVE_OUT];  // each wave's pooled codes of a tile
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int n = lane & 15, g = lane >> 4;
   const int py = 2 * (n >> 3) + ((n >> 1) & 1), px = 2 * ((n >> 2) & 1) + (n & 1);  // A row n (as the float kernel)
   const int Ho = H / 2, Wo = W / 2;
+  int8_t* cw = codes_l[wave] + ((g >> 1) * (C0_TX / 2) + (g & 1)) * C0_OUT + n;  // as the float kernel
 
   v4i wa;  // B operand: channel n, kernel row g, (kx, c) = (i >> 2, i & 3) for byte i
   {
@@ -373,16 +375,24 @@ __global__ __launch_bounds__(256, 4) void ultra_conv0_int_mfma_kernel(const uint
   const v4i ones = v4i{0x01010101, 0x01010101, 0x01010101, 0x01010101};
   const int wsum = 128 * __builtin_amdgcn_mfma_i32_16x16x64_i8(ones, wa, v4i{0, 0, 0, 0}, 0, 0, 0)[0];
   const int ic = inc[n], bc = bias[n];
+  asm volatile("" ::"v"(ic), "v"(bc));  // both arrive before the loop (see the float kernel)
 
   const int tiles_y = (H + C0_TY - 1) / C0_TY, tiles_x = (W + C0_TX - 1) / C0_TX;
   const int ntiles = B * tiles_y * tiles_x;
   const int64_t HW = (int64_t)H * W;
+  struct TPos {
+    int b, ty, tx;
+  };
+  auto tpos = [&](int t) __attribute__((always_inline)) {
+    const int row = t / tiles_x;
+    return TPos{row / tiles_y, row - (row / tiles_y) * tiles_y, t - row * tiles_x};
+  };
   // this thread's halo quad (as the float kernel): per channel 4 bytes, staged as x - 128 in 4-channel pixels
   const int qy = tid / (C0_HX / 4), qx = tid - qy * (C0_HX / 4);
   uint32_t xin[3];
-  auto load_tile = [&](int t) __attribute__((always_inline)) {
+  auto load_tile = [&](const TPos& p) __attribute__((always_inline)) {
     if (tid >= C0_QUADS) return;
-    const int tx0 = (t % tiles_x) * C0_TX, ty0 = ((t / tiles_x) % tiles_y) * C0_TY, b = t / (tiles_x * tiles_y);
+    const int b = p.b, ty0 = p.ty * C0_TY, tx0 = p.tx * C0_TX;
     const uint8_t* base = img + (int64_t)b * 3 * HW;
     const int y = ty0 - 1 + qy, x = tx0 - 4 + 4 * qx;
     const bool row = y >= 0 && y < H;
@@ -420,15 +430,37 @@ __global__ __launch_bounds__(256, 4) void ultra_conv0_int_mfma_kernel(const uint
   const TileWalk tw = tile_walk(ntiles);
   int t = tw.lo + tw.slot;
   if (t >= tw.hi) return;
-  load_tile(t);
+  TPos cur = tpos(t);
+  const TPos step = tpos(tw.team);
+  auto advance = [&](TPos p) __attribute__((always_inline)) {
+    p.tx += step.tx;
+    if (p.tx >= tiles_x) p.tx -= tiles_x, p.ty += 1;
+    p.ty += step.ty;
+    if (p.ty >= tiles_y) p.ty -= tiles_y, p.b += 1;
+    p.b += step.b;
+    return p;
+  };
+  load_tile(cur);
   stage_tile(smem[0]);
   __syncthreads();
+  auto flush = [&](int b, int ty0, int tx0) __attribute__((always_inline)) {  // as the float kernel
+    __builtin_amdgcn_wave_barrier();
+    if (lane < 32) {
+      const int yo = ((ty0 + 4 * wave) >> 1) + (lane >> 4), xo = (tx0 >> 1) + (lane & 15);
+      const uint4 v = *reinterpret_cast<const uint4*>(codes_l[wave] + lane * C0_OUT);
+      if (yo < Ho && xo < Wo) *reinterpret_cast<uint4*>(out + (((int64_t)b * Ho + yo) * Wo + xo) * C0_OUT) = v;
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
+  int pb = 0, pty = 0, ptx = 0;
   for (int it = 0; t < tw.hi; t += tw.team, ++it) {
     const int8_t* buf = smem[it & 1];
     const int tn = t + tw.team;
-    if (tn < tw.hi) load_tile(tn);
-    const int tx0 = (t % tiles_x) * C0_TX, ty0 = ((t / tiles_x) % tiles_y) * C0_TY, b = t / (tiles_x * tiles_y);
-    const int yo = ((ty0 + 4 * wave) >> 1) + (g >> 1);
+    const TPos nxt = advance(cur);
+    if (tn < tw.hi) load_tile(nxt);
+    if (it > 0) flush(pb, pty, ptx);
+    pb = cur.b, pty = cur.ty * C0_TY, ptx = cur.tx * C0_TX;
+    cur = nxt;
     // A fragment: pixels px .. px + 3 of kernel row g (group 3 re-reads row 2: zero weights)
     const int8_t* bb = buf + ((4 * wave + py + (g < 3 ? g : 2)) * C0_HX + px + 3) * 4;
 #pragma unroll
@@ -445,16 +477,14 @@ __global__ __launch_bounds__(256, 4) void ultra_conv0_int_mfma_kernel(const uint
       for (int q = 0; q < 2; ++q) {
         const int mx = max(max(acc[q][0], acc[q][1]), max(acc[q][2], acc[q][3]));
         const int mn = min(min(acc[q][0], acc[q][1]), min(acc[q][2], acc[q][3]));
-        const int code = int_code((ic < 0 ? mn : mx) + wsum, ic, bc, sbits, levels);
-        const int xo = ((tx0 + 4 * (pq + q)) >> 1) + (g & 1);
-        const uint32_t word = pack_quad(code);
-        if ((n & 3) == 0 && yo < Ho && xo < Wo)
-          *reinterpret_cast<uint32_t*>(out + (((int64_t)b * Ho + yo) * Wo + xo) * C0_OUT + n) = word;
+        cw[2 * (pq + q) * C0_OUT] = (int8_t)int_code((ic < 0 ? mn : mx) + wsum, ic, bc, sbits, levels);
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
     if (tn < tw.hi) stage_tile(smem[(it + 1) & 1]);
     __syncthreads();
   }
+  flush(pb, pty, ptx);
 }
 
 // ---- layers 1..8: implicit GEMM conv on MFMA ------------------------------------------------------
