@@ -160,52 +160,34 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const float* __restrict__ 
 // ---- split fp16 input (the fused block path) --------------------------------------------------------
 // q, k, v arrive pre-scaled and pre-split by the qkv GEMM (qvit_gemm_qkv_split): hi and lo planes of
 // layout [B][3H][N][64] fp16, so a key block's four LDS images (K hi/lo, V hi/lo; 32 rows x 128 B) are
-// copied by LDS-DMA straight from global memory, the swizzle applied on the source side, with no register
-// staging and no conversion in this kernel.
-// One workgroup of SW = 8 waves per CU (2 per SIMD), ST = 3 query tiles per wave (SQG = 384 queries per unit:
-// a ViT-L head's 577 queries are two units, 24 + 13 tiles), and a ring of SR = 8 blocks (128 KiB): SR - 1
-// blocks in flight, each feeding 8 waves' work. Three tiles per wave leave the registers for the V
-// fragments of a block to be issued before its softmax (attend's VEARLY).
-constexpr int SW = 8;                 // waves
-constexpr int ST = 3;                 // query tiles per wave
-constexpr int SR = 8;                 // ring blocks
-constexpr int SQG = SW * ST * 16;     // queries per unit (384)
+// copied by LDS-DMA straight from global memory, the swizzle applied on the source side. A ring of
+// SRING blocks keeps SRING - 1 blocks (48 KiB per workgroup) in flight: a head's keys stream while the
+// previous block is computed, with no register staging and no conversion in this kernel.
+constexpr int SRING = 4;
 
-// wait until block p landed for this wave (2 DMAs per wave per block; `ahead` younger blocks in flight, at
-// most SR - 2) and every wave is done with block p - 1
-QVIT_DEV void split_sync(int ahead) {
-  switch (ahead < SR - 2 ? ahead : SR - 2) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(10)\n\ts_barrier" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory"); break;
-  }
+template <int N_>
+QVIT_DEV void block_sync() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N_) : "memory");
 }
-static_assert(SR - 2 == 6, "split_sync's cases");
 
-// Persistent: the workgroups walk the units (image, head, group of <= SQG queries). Each unit is a run of
-// ring blocks in one stream: nqb query blocks (64 queries = 4 tiles: hi and lo images in the K layout) and
-// then nkb key blocks. Block p + SR - 1 is issued as soon as block p is waited for, across unit boundaries,
-// so the next unit's queries and first keys land while the current unit finishes. Every global load of the
-// loop is an LDS-DMA (the quantizer scalars are read before the stream starts), so the only vmcnt waits are
-// the counted stage waits; the output stores of a unit's epilogue do join the count and are drained by the
-// next wait. Tile i of wave w' (w' = wave rotated by unit) is query tile SW i + w' of the unit: query block
-// 2 i + (w' >> 2), rows 16 (w' & 3) .. + 15.
+// Persistent: workgroup w walks the units (image, head, group of <= QG queries) w, w + grid, ... Each
+// unit is a run of ring blocks in one stream: nqb query blocks (64 queries: hi and lo images in the K
+// layout, wave w reads its tile from each) and then nkb key blocks. Block p + 3 is issued as soon as
+// block p is waited for, across unit boundaries, so the next unit's queries and first keys land while the
+// current unit finishes. Every global load of the loop is an LDS-DMA (the quantizer scalars are read
+// before the stream starts), so the only vmcnt waits are the counted stage waits; the output stores of a
+// unit's epilogue do join the count and are drained by the next wait.
 constexpr int QB = 64;  // queries per query block
-constexpr int TBL_BYTES = 16384;  // int8 epilogue code table (<= 2046 buckets)
+constexpr int TBL_BYTES = 16384;  // int8 epilogue code table (<= 2046 buckets): 2 x (64 + 16) KiB per CU
 
 template <int OUT>
-__global__ __launch_bounds__(SW * 64, 1) void attn_split_kernel(const _Float16* __restrict__ hi,
-                                                                const _Float16* __restrict__ lo, int N, int H,
-                                                                int nunits, float scale, float in_scale,
-                                                                void* __restrict__ out, int64_t ldo, int out_qtype,
-                                                                const float* out_d, const float* out_qm,
-                                                                const float* out_t, int out_levels,
-                                                                const int8_t* __restrict__ epi_table) {
-  __shared__ __attribute__((aligned(16))) int8_t smem[SR * STAGE + (OUT == 1 ? TBL_BYTES : 0)];
+__global__ __launch_bounds__(256, 2) void attn_split_kernel(const _Float16* __restrict__ hi,
+                                                            const _Float16* __restrict__ lo, int N, int H, int nunits,
+                                                            float scale, float in_scale, void* __restrict__ out,
+                                                            int64_t ldo, int out_qtype, const float* out_d,
+                                                            const float* out_qm, const float* out_t, int out_levels,
+                                                            const int8_t* __restrict__ epi_table) {
+  __shared__ __attribute__((aligned(16))) int8_t smem[SRING * STAGE + (OUT == 1 ? TBL_BYTES : 0)];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -219,8 +201,8 @@ __global__ __launch_bounds__(SW * 64, 1) void attn_split_kernel(const _Float16* 
     if (epi_table != nullptr) {  // the code table -> LDS, once per workgroup
       const EpiTableHdr hd = *reinterpret_cast<const EpiTableHdr*>(epi_table);
       if (hd.valid != 0 && hd.nb >= 1 && 16 + 8 * hd.nb <= TBL_BYTES) {
-        int8_t* tl = smem + SR * STAGE;
-        for (int k = tid; k < (16 + 8 * hd.nb + 15) / 16; k += SW * 64)
+        int8_t* tl = smem + SRING * STAGE;
+        for (int k = tid; k < (16 + 8 * hd.nb + 15) / 16; k += 256)
           reinterpret_cast<uint4*>(tl)[k] = reinterpret_cast<const uint4*>(epi_table)[k];
         tb = EpiLds{tl + sizeof(EpiTableHdr), hd.c0, hd.inv_w, epi_top(hd.nb)};
       }
@@ -229,13 +211,10 @@ __global__ __launch_bounds__(SW * 64, 1) void attn_split_kernel(const _Float16* 
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): nothing of the compiler's own is pending below
   const bool st16 = ((ldo & 15) == 0) && ((((uintptr_t)out) & 15) == 0);
 
-  const int ngroups = (N + SQG - 1) / SQG;
+  const int ngroups = (N + QG - 1) / QG;
+  const int nqb = (N < QG ? (N + QB - 1) / QB : QG / QB);
   const int nkb = (N + KB - 1) / KB;
-  // query blocks of unit group grp: those holding queries < N (at most SQG / QB)
-  auto nqb_of = [&](int grp) {
-    const int rest = N - grp * SQG;
-    return rest >= SQG ? SQG / QB : (rest + QB - 1) / QB;
-  };
+  const int per = nqb + nkb;
   // units of this workgroup: with a grid that is a multiple of 8, XCD x (blocks x, x + 8, ...) owns a contiguous
   // unit range, so the query groups of one (image, head) stream the same K / V through one XCD's L2 instead of
   // fetching it once per XCD; otherwise units blockIdx + j * grid
@@ -249,57 +228,55 @@ __global__ __launch_bounds__(SW * 64, 1) void attn_split_kernel(const _Float16* 
     uhi = ulo + per8 + (xcd < rem ? 1 : 0);
   }
   const int my_units = (uhi - ulo - slot + team - 1) / team;  // unit j: ulo + slot + j * team
+  const int total = my_units * per;
   const int64_t plane = (int64_t)N * HD;
 
   const uint32_t lds0 = lds_addr(smem);
-  // the stream position of block p: (unit j, index in the unit); units differ in length (query blocks), so
-  // the issue side walks its own cursor
-  int ij = 0, iidx = 0, issue_slot = 0;  // the next block to issue: unit j, index in the unit, ring slot
-  auto issue_next = [&]() {
-    const int unit = ulo + slot + ij * team;
+  // DMA of stream block p into ring slot p % SRING
+  auto issue = [&](int p) {
+    const int j = p / per, idx = p - j * per;
+    const int unit = ulo + slot + j * team;
     const int grp = unit % ngroups, bh = unit / ngroups;
     const int h = bh % H, b = bh / H;
-    const int nqb = nqb_of(grp);
     const int64_t qoff = ((int64_t)b * 3 * H + h) * plane;
-    const uint32_t sbase = __builtin_amdgcn_readfirstlane(lds0 + (unsigned)issue_slot * STAGE);
-    if (iidx < nqb) {  // query block: wave w stages rows 8w .. 8w + 7 of the hi and the lo image (K layout)
+    const uint32_t base = __builtin_amdgcn_readfirstlane(lds0 + (p & (SRING - 1)) * STAGE);
+    if (idx < nqb) {  // query block: rows 16w .. 16w+15 of the hi and lo images (K layout)
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc) {
+        const int r = 16 * wave + 8 * pc + (lane >> 3);
+        int q = grp * QG + idx * QB + r;
+        q = q < N ? q : N - 1;
+        const int kc = ((lane & 7) ^ ((r >> 1) & 7)) << 4;
+        const int64_t e = qoff + (int64_t)q * HD;
+        const uint32_t d = base + (16 * wave + 8 * pc) * 128;
+        dma16(reinterpret_cast<const int8_t*>(hi + e) + kc, __builtin_amdgcn_readfirstlane(d));
+        dma16(reinterpret_cast<const int8_t*>(lo + e) + kc, __builtin_amdgcn_readfirstlane(d + QB * 128));
+      }
+    } else {          // key block: rows 8w .. 8w+7 of K hi, K lo, V hi, V lo
+      const int kb = idx - nqb;
       const int r = 8 * wave + (lane >> 3);
-      int q = grp * SQG + iidx * QB + r;
-      q = q < N ? q : N - 1;
-      const int kc = ((lane & 7) ^ ((r >> 1) & 7)) << 4;
-      const int64_t e = qoff + (int64_t)q * HD;
-      const uint32_t d = sbase + 8 * wave * 128;
-      dma16(reinterpret_cast<const int8_t*>(hi + e) + kc, __builtin_amdgcn_readfirstlane(d));
-      dma16(reinterpret_cast<const int8_t*>(lo + e) + kc, __builtin_amdgcn_readfirstlane(d + QB * 128));
-    } else {          // key block: waves 0-3 stage K hi / lo rows 8 (w & 3) .. + 7, waves 4-7 the V rows
-      const int kb = iidx - nqb;
-      const int r = 8 * (wave & 3) + (lane >> 3);
       const int sc = lane & 7;
       int key = kb * KB + r;
       key = key < N ? key : N - 1;  // keys past N: a valid row, masked out of the softmax
-      const uint32_t d = sbase + (wave & 3) * 1024;
-      if (wave < 4) {
-        const int kc = (sc ^ ((r >> 1) & 7)) << 4;
-        const int64_t ke = qoff + H * plane + (int64_t)key * HD;
-        dma16(reinterpret_cast<const int8_t*>(hi + ke) + kc, __builtin_amdgcn_readfirstlane(d));
-        dma16(reinterpret_cast<const int8_t*>(lo + ke) + kc, __builtin_amdgcn_readfirstlane(d + IMG));
-      } else {
-        const int vb = (((sc >> 1) ^ ((r >> 1) & 3)) << 5) | ((sc & 1) << 4);
-        const int64_t ve = qoff + 2 * H * plane + (int64_t)key * HD;
-        dma16(reinterpret_cast<const int8_t*>(hi + ve) + vb, __builtin_amdgcn_readfirstlane(d + 2 * IMG));
-        dma16(reinterpret_cast<const int8_t*>(lo + ve) + vb, __builtin_amdgcn_readfirstlane(d + 3 * IMG));
-      }
+      const int kc = (sc ^ ((r >> 1) & 7)) << 4;
+      const int vb = (((sc >> 1) ^ ((r >> 1) & 3)) << 5) | ((sc & 1) << 4);
+      const int64_t ke = qoff + H * plane + (int64_t)key * HD;
+      const int64_t ve = ke + H * plane;
+      const uint32_t d = base + wave * 1024;
+      dma16(reinterpret_cast<const int8_t*>(hi + ke) + kc, __builtin_amdgcn_readfirstlane(d));
+      dma16(reinterpret_cast<const int8_t*>(lo + ke) + kc, __builtin_amdgcn_readfirstlane(d + IMG));
+      dma16(reinterpret_cast<const int8_t*>(hi + ve) + vb, __builtin_amdgcn_readfirstlane(d + 2 * IMG));
+      dma16(reinterpret_cast<const int8_t*>(lo + ve) + vb, __builtin_amdgcn_readfirstlane(d + 3 * IMG));
     }
-    issue_slot = (issue_slot + 1) & (SR - 1);
-    if (++iidx == nqb + nkb) iidx = 0, ++ij;
   };
-  int issued = 0, p = 0;  // blocks issued; the block waited for next
-  auto more = [&]() { return ij < my_units; };
-  // block p landed (issued - p - 1 younger blocks in flight); block p + SR - 1 takes the slot of p - 1, free
-  // once every wave passed this barrier
-  auto sync = [&]() {
-    split_sync(issued - p - 1);
-    if (more()) issue_next(), ++issued;
+  // block p landed for every wave (4 DMAs per wave per block; up to two younger blocks in flight) and
+  // every wave is done with block p - 1, whose slot block p + 3 takes
+  auto sync = [&](int p) {
+    const int ahead = total - 1 - p;
+    if (ahead >= 2) block_sync<8>();
+    else if (ahead == 1) block_sync<4>();
+    else block_sync<0>();
+    if (p + 3 < total) issue(p + 3);
   };
 
   int koffs[2][2], voffs[4];
@@ -307,42 +284,39 @@ __global__ __launch_bounds__(SW * 64, 1) void attn_split_kernel(const _Float16* 
   const float sl2 = scale * LOG2E / (in_scale * in_scale);
 
   Stamps sp;
-  for (int k = 0; k < SR - 1 && more(); ++k) issue_next(), ++issued;
+  for (int p = 0; p < 3 && p < total; ++p) issue(p);
+  int p = 0;
   for (int j = 0; j < my_units; ++j) {
     const int unit = ulo + slot + j * team;
     const int grp = unit % ngroups, bh = unit / ngroups;
     const int h = bh % H, b = bh / H;
-    const int q0 = grp * SQG;
-    const int nqb = nqb_of(grp);
-    const int wr = (wave + unit) & (SW - 1);  // the waves owning the longest tile lists rotate by unit
-    h8 qh[ST][2], ql[ST][2];
-#pragma unroll
-    for (int i = 0; i < ST; ++i) qh[i][0] = qh[i][1] = ql[i][0] = ql[i][1] = h8{};
-#pragma unroll
-    for (int qb = 0; qb < SQG / QB; ++qb) {
-      if (qb < nqb) {
-        sp.mark(4);
-        sync();
-        sp.mark(0);
-        if ((qb & 1) == (wr >> 2)) {  // wave-uniform: this block holds the wave's tile qb >> 1
-          const int8_t* st = smem + (p & (SR - 1)) * STAGE;
-#pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            const int off = koff(16 * (wr & 3) + fr, g + 4 * c);
-            qh[qb >> 1][c] = lds_h8(st, off);
-            ql[qb >> 1][c] = lds_h8(st + QB * 128, off);
-          }
-        }
-        ++p;
-      }
-    }
+    const int q0 = grp * QG;
+    const int wr = (wave + unit) & (NWAVES - 1);  // the wave owning a 4th tile rotates by unit
+    h8 qh[QTW][2], ql[QTW][2];
     int nt = 0;
 #pragma unroll
-    for (int i = 0; i < ST; ++i) nt += (q0 + 16 * (SW * i + wr) < N) ? 1 : 0;
-    float m[ST], l[ST];
-    f4 o[ST][4];
+    for (int i = 0; i < QTW; ++i) {
+      if (i < nqb) {
+        sp.mark(4);
+        sync(p);
+        sp.mark(0);
+        const int8_t* st = smem + (p & (SRING - 1)) * STAGE;
 #pragma unroll
-    for (int i = 0; i < ST; ++i) {
+        for (int c = 0; c < 2; ++c) {
+          const int off = koff(16 * wr + fr, g + 4 * c);
+          qh[i][c] = lds_h8(st, off);
+          ql[i][c] = lds_h8(st + QB * 128, off);
+        }
+        ++p;
+      } else {  // no such query block: zeros (the tile is skipped or discarded)
+        qh[i][0] = qh[i][1] = ql[i][0] = ql[i][1] = h8{};
+      }
+      nt += (i < nqb && q0 + 16 * (wr + NWAVES * i) < N) ? 1 : 0;
+    }
+    float m[QTW], l[QTW];
+    f4 o[QTW][4];
+#pragma unroll
+    for (int i = 0; i < QTW; ++i) {
       m[i] = -INFINITY;
       l[i] = 0.f;
 #pragma unroll
@@ -350,15 +324,15 @@ __global__ __launch_bounds__(SW * 64, 1) void attn_split_kernel(const _Float16* 
     }
     sp.mark(5);
     for (int kb = 0; kb < nkb; ++kb, ++p) {
-      sync();
+      sync(p);
       sp.mark(0);
-      attend<ST, IMG, true>(nt, (kb + 1) * KB > N, smem + (p & (SR - 1)) * STAGE, qh, ql, m, l, o, koffs, voffs,
-                            kb * KB + 4 * g, N, sl2, sp);
+      attend_n(nt, (kb + 1) * KB > N, smem + (p & (SRING - 1)) * STAGE, qh, ql, m, l, o, koffs, voffs,
+               kb * KB + 4 * g, N, sl2, sp);
     }
-    bool tv[ST];
+    bool tv[QTW];
 #pragma unroll
-    for (int i = 0; i < ST; ++i) tv[i] = i < nt;
-    attend_store<OUT, ST>(tv, l, o, wr, SW, q0, N, b, h, in_scale, out, ldo, qp, tb, st16);
+    for (int i = 0; i < QTW; ++i) tv[i] = i < nt;
+    attend_store<OUT, QTW>(tv, l, o, wr, NWAVES, q0, N, b, h, in_scale, out, ldo, qp, tb, st16);
   }
   sp.mark(4);
   sp.flush();
@@ -421,7 +395,7 @@ extern "C" int qvit_attention_split(const void* qkv_hi, const void* qkv_lo, int6
     return QVIT_EINVAL;
   }
   if (B == 0) return QVIT_OK;
-  const int64_t ngroups = (N + SQG - 1) / SQG;
+  const int64_t ngroups = (N + QG - 1) / QG;
   const int64_t nblk = B * H * ngroups;
   if (nblk > INT32_MAX) return QVIT_EINVAL;
   const _Float16* hi = reinterpret_cast<const _Float16*>(qkv_hi);
@@ -433,13 +407,13 @@ extern "C" int qvit_attention_split(const void* qkv_hi, const void* qkv_lo, int6
       n = 256;
     return n;
   }();
-  const int64_t grid = std::min<int64_t>(nblk, (int64_t)cus);  // one resident workgroup per CU
+  const int64_t grid = std::min<int64_t>(nblk, 2 * (int64_t)cus);  // two resident workgroups per CU
   if (out_mode == QVIT_ATT_F32)
-    hipLaunchKernelGGL(attn_split_kernel<0>, dim3((unsigned)grid), dim3(SW * 64), 0, stream, hi, lo, (int)N, (int)H,
+    hipLaunchKernelGGL(attn_split_kernel<0>, dim3((unsigned)grid), dim3(256), 0, stream, hi, lo, (int)N, (int)H,
                        (int)nblk, scale, in_scale, out, ldo, out_qtype, out_d, out_qm, out_t, out_levels,
                        nullptr);
   else
-    hipLaunchKernelGGL(attn_split_kernel<1>, dim3((unsigned)grid), dim3(SW * 64), 0, stream, hi, lo, (int)N, (int)H,
+    hipLaunchKernelGGL(attn_split_kernel<1>, dim3((unsigned)grid), dim3(256), 0, stream, hi, lo, (int)N, (int)H,
                        (int)nblk, scale, in_scale, out, ldo, out_qtype, out_d, out_qm, out_t, out_levels,
                        reinterpret_cast<const int8_t*>(epi_table));
   return qvit_hip_status(hipGetLastError());
