@@ -14,6 +14,7 @@ layers). Anything else (training mode, CPU tensors, non-reference layer stacks) 
 """
 from __future__ import annotations
 
+import contextlib
 from typing import Optional
 
 import torch
@@ -90,6 +91,17 @@ def _conv_stack(w_bit=W_BIT, a_bit=A_BIT):
             mods.append(nn.MaxPool2d(2, stride=2))
     mods.append(conv2d_q(64, 36, kernel_size=1, stride=1, padding=0))
     return nn.Sequential(*mods)
+
+
+@contextlib.contextmanager
+def _aten_batch_norm():
+    """BatchNorm2d on ATen's own kernels: torch routes an fp32 batch norm to MIOpen while cudnn is enabled."""
+    prev = torch.backends.cudnn.enabled
+    torch.backends.cudnn.enabled = False
+    try:
+        yield
+    finally:
+        torch.backends.cudnn.enabled = prev
 
 
 def _round_up(v, m):
@@ -188,12 +200,8 @@ class UltraNetQua(nn.Module):
         library kernel is on the path). Any image size, training mode included."""
         img_size = x.shape[-2:]
         yolo_out = []
-        prev = torch.backends.cudnn.enabled
-        torch.backends.cudnn.enabled = False
-        try:
+        with _aten_batch_norm():
             x = self.layers(x)
-        finally:
-            torch.backends.cudnn.enabled = prev
         x = self.yololayer(x, img_size)
         yolo_out.append(x)
         if self.training:
@@ -230,9 +238,10 @@ def random_ultranet(seed: int = 0, device: Optional[torch.device] = None, calib_
                 mod.bias.copy_(torch.rand(n, generator=g) * 0.4 + 0.3)
         m = m.to(device).eval()
         x = synthetic_images_u8(calib_batch, img_size, seed + 1, device)
-        for mod in m.layers:
-            if isinstance(mod, nn.BatchNorm2d):
-                mod.running_mean.copy_(x.mean(dim=(0, 2, 3)))
-                mod.running_var.copy_(x.var(dim=(0, 2, 3)).clamp_min(1e-3))
-            x = mod(x)
+        with _aten_batch_norm():
+            for mod in m.layers:
+                if isinstance(mod, nn.BatchNorm2d):
+                    mod.running_mean.copy_(x.mean(dim=(0, 2, 3)))
+                    mod.running_var.copy_(x.var(dim=(0, 2, 3)).clamp_min(1e-3))
+                x = mod(x)
     return m
