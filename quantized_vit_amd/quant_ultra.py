@@ -145,6 +145,12 @@ def conv2d_Q_fn(w_bit):
             self.quantize_fn = weight_quantize_fn(w_bit=w_bit)
             self._codes = _PackedCodes()
 
+        def prepare(self):
+            """Packs the weight codes now (cached per weight version; see QuantizeMixin.prepare)."""
+            if _codes_path(self.w_bit) and self.weight.is_cuda:
+                self._codes.get(self.weight, self.bias, self.w_bit)
+            return self
+
         def forward(self, input, order=None):
             if _codes_path(self.w_bit):
                 _check_gpu(input, "input")
@@ -211,6 +217,12 @@ def linear_Q_fn(w_bit):
             self.w_bit = w_bit
             self.quantize_fn = weight_quantize_fn(w_bit=w_bit)
             self._codes = _PackedCodes()
+
+        def prepare(self):
+            """Packs the weight codes now (cached per weight version; see QuantizeMixin.prepare)."""
+            if _codes_path(self.w_bit) and self.weight.is_cuda:
+                self._codes.get(self.weight, self.bias, self.w_bit)
+            return self
 
         def forward(self, input):
             if not _codes_path(self.w_bit):
