@@ -111,6 +111,7 @@ typedef _Float16 c0h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 c0h4 __attribute__((ext_vector_type(4)));
 typedef float c0f4 __attribute__((ext_vector_type(4)));
 typedef int c0i4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 QVIT_DEV float fmax_nn(float a, float b) { return __builtin_elementwise_maximum(a, b); }
 QVIT_DEV float fmin_nn(float a, float b) { return __builtin_elementwise_minimum(a, b); }
@@ -540,15 +541,25 @@ struct ConvGeo {
 // minimum resident workgroups per CU by input width (register budget): CIN 32 at 3 instead of 2 (168 VGPRs, no
 // spills): conv2 114-116 -> 96-98 us at b256 (profiles/r03_conv0_occupancy_ab.txt)
 constexpr int UC_MINB16 = 2, UC_MINB32 = 3;
-template <int CIN, int KS, int COUT, int POOL, int OUT>
-__global__ __launch_bounds__(256, CIN == 32 ? UC_MINB32 : CIN == 16 ? UC_MINB16 : 2) void ultra_conv_kernel(const int8_t* __restrict__ in, int B, int H, int W,
+// zeros for the LDS-DMA of halo pixels outside the image
+__device__ __attribute__((aligned(16))) int4 qvit_ultra_zero16 = {0, 0, 0, 0};
+
+// STG (pooled code layers whose output rows are whole 16-B groups, cout == COUT): the halo of tile t + 1 is
+// LDS-DMA'd into the second halo buffer while tile t computes (no register staging: zeros for pixels outside
+// the image come from a zero line), and the pooled codes leave through a per-wave LDS image as one 16-B
+// buffer store per lane, so each wave has exactly one vector-memory operation younger than the halo it waits for.
+template <int CIN, int KS, int COUT, int POOL, int OUT, bool STG>
+__global__ __launch_bounds__(256, STG ? 2 : CIN == 32 ? UC_MINB32 : CIN == 16 ? UC_MINB16 : 2) void ultra_conv_kernel(const int8_t* __restrict__ in, int B, int H, int W,
                                                             const int8_t* __restrict__ wcodes, int kpad_in,
                                                             float den, const float* __restrict__ alpha,
                                                             const float* __restrict__ shift, float levels,
                                                             int cout_real, void* __restrict__ out, int ldo,
                                                             int sbits) {
   using G = ConvGeo<CIN, KS, COUT>;
-  __shared__ __attribute__((aligned(16))) int8_t smem[G::LDS];
+  constexpr bool STAGED = STG && POOL != 0 && OUT != 1;
+  constexpr int HALO16 = (G::HALO + 15) / 16 * 16;
+  constexpr int WOUT = 2 * (TS / 2) * COUT;  // a wave's pooled codes per tile (2 rows x 8 columns)
+  __shared__ __attribute__((aligned(16))) int8_t smem[COUT * G::WSTR + HALO16 + (STAGED ? HALO16 + 4 * WOUT : 0)];
   int8_t* wl = smem;
   int8_t* halo = smem + COUT * G::WSTR;
   const int tid = threadIdx.x;
@@ -591,11 +602,116 @@ __global__ __launch_bounds__(256, CIN == 32 ? UC_MINB32 : CIN == 16 ? UC_MINB16 
     shs[ct] = (SW && OUT == 0 && o < cout_real) ? shift[o] : 0.f;
     iincs[ct] = (SW && OUT == 2 && o < cout_real) ? reinterpret_cast<const int*>(alpha)[o] : 0;
     ibiass[ct] = (SW && OUT == 2 && o < cout_real) ? reinterpret_cast<const int*>(shift)[o] : 0;
+    // arrived before the loop: a first use inside it would carry a compiler vmcnt(0) that drains the halo DMA
+    if (STG) asm volatile("" ::"v"(als[ct]), "v"(shs[ct]), "v"(iincs[ct]), "v"(ibiass[ct]));
   }
 
   const int tiles_y = (H + TS - 1) / TS, tiles_x = (W + TS - 1) / TS;
   const int64_t ntiles = (int64_t)B * tiles_y * tiles_x;
   const TileWalk tw = tile_walk((int)ntiles);
+
+  // the implicit-GEMM contraction of one tile from the halo image hb
+  auto conv_tile = [&](const int8_t* hb, v4i (&acc)[4][G::NCT]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt)
+#pragma unroll
+      for (int ct = 0; ct < G::NCT; ++ct) acc[pt][ct] = v4i{0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < G::KPAD / 64; ++j) {
+      const int kk = 64 * j + 16 * g;
+      const int tap = kk / CIN, c0 = kk % CIN;
+      const bool kv = tap < KS * KS;
+      const int kty = kv ? tap / KS : 0, ktx = kv ? tap % KS : 0;
+      v4i a[G::NCT], bf[4];
+#pragma unroll
+      for (int ct = 0; ct < G::NCT; ++ct) a[ct] = *reinterpret_cast<const v4i*>(wl + (16 * ct + p) * G::WSTR + kk);
+#pragma unroll
+      for (int pt = 0; pt < 4; ++pt) {
+        const int hy = 4 * wave + py + kty, hx = 4 * pt + px + ktx;
+        bf[pt] = *reinterpret_cast<const v4i*>(hb + (hy * G::HT + hx) * CIN + c0);
+        if (!kv) bf[pt] = v4i{0, 0, 0, 0};
+      }
+#pragma unroll
+      for (int pt = 0; pt < 4; ++pt)
+#pragma unroll
+        for (int ct = 0; ct < G::NCT; ++ct)
+          acc[pt][ct] = SW ? __builtin_amdgcn_mfma_i32_16x16x64_i8(bf[pt], a[ct], acc[pt][ct], 0, 0, 0)
+                           : __builtin_amdgcn_mfma_i32_16x16x64_i8(a[ct], bf[pt], acc[pt][ct], 0, 0, 0);
+    }
+  };
+
+  if constexpr (STAGED) {
+    int8_t* halo1 = halo + HALO16;
+    int8_t* codes_w = halo1 + HALO16 + wave * WOUT;
+    // DMA of tile t's halo into hb: 1-KiB pieces i = wave, wave + 4, ...; lane L of piece i fills bytes
+    // 1024 i + 16 L of the image (hy, hx, channel chunk), past the image end the lanes are masked off
+    constexpr int NPIECE = (G::HALO + 1023) / 1024;
+    auto issue_halo = [&](int t, int8_t* hb) __attribute__((always_inline)) {
+      const int row = t / tiles_x, b = row / tiles_y;
+      const int tx0 = (t - row * tiles_x) * TS, ty0 = (row - b * tiles_y) * TS;
+      const uint32_t lb = lds_addr(hb);
+#pragma unroll
+      for (int i = 0; i < NPIECE; ++i) {
+        if ((i & 3) != wave) continue;  // wave-uniform
+        const int o = 1024 * i + 16 * lane;
+        if (o < G::HALO) {
+          const int hy = o / (G::HT * CIN), r = o - hy * (G::HT * CIN);
+          const int hx = r / CIN, c = r - hx * CIN;
+          const int y = ty0 - KS / 2 + hy, x = tx0 - KS / 2 + hx;
+          const void* src = (y >= 0 && y < H && x >= 0 && x < W)
+                                ? static_cast<const void*>(in + (((int64_t)b * H + y) * W + x) * CIN + c)
+                                : static_cast<const void*>(&qvit_ultra_zero16);
+          dma16(src, __builtin_amdgcn_readfirstlane(lb + 1024 * i));
+        }
+      }
+    };
+    const int Ho = H / 2, Wo = W / 2;
+    // this lane's code byte for (patch pt, channel tile ct): pooled row g >> 1, column 2 pt + (g & 1), channel
+    // 16 ct + p; the flush: lane l stores channels 16 (l % (COUT / 16)) .. + 15 of pooled pixel l / (COUT / 16)
+    int8_t* cw = codes_w + ((g >> 1) * (TS / 2) + (g & 1)) * COUT + p;
+    constexpr int CG = COUT / 16;  // 16-B groups per pooled pixel
+    int t = tw.lo + tw.slot;
+    if (t < tw.hi) issue_halo(t, halo);
+    for (int it = 0; t < tw.hi; t += tw.team, ++it) {
+      // tile t's halo landed for every wave (the only younger operation of a wave is its previous flush store),
+      // every wave is done with the other buffer (the previous tile) and with its codes image
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      if (it == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(1)\n\ts_barrier" ::: "memory");
+      const int tn = t + tw.team;
+      if (tn < tw.hi) issue_halo(tn, (it & 1) ? halo : halo1);
+      const int row = t / tiles_x, b = row / tiles_y;
+      const int tx0 = (t - row * tiles_x) * TS, ty0 = (row - b * tiles_y) * TS;
+      v4i acc[4][G::NCT];
+      conv_tile((it & 1) ? halo1 : halo, acc);
+#pragma unroll
+      for (int pt = 0; pt < 4; ++pt)
+#pragma unroll
+        for (int ct = 0; ct < G::NCT; ++ct) {
+          const v4i v = acc[pt][ct];
+          const int vmax = max(max(v[0], v[1]), max(v[2], v[3]));
+          const int vmin = min(min(v[0], v[1]), min(v[2], v[3]));
+          const int code = (OUT == 2) ? int_code(iincs[ct] < 0 ? vmin : vmax, iincs[ct], ibiass[ct], sbits, (int)levels)
+                                      : act_code((float)(als[ct] < 0.f ? vmin : vmax) / den, als[ct], shs[ct], levels);
+          cw[2 * pt * COUT + 16 * ct] = (int8_t)code;
+        }
+      __builtin_amdgcn_wave_barrier();
+      {
+        const int q = lane / CG, cc = lane - q * CG;  // pooled pixel q (row q >> 3, column q & 7), group cc
+        const int yo = ((ty0 + 4 * wave) >> 1) + (q >> 3), xo = (tx0 >> 1) + (q & 7);
+        const bool ok = lane < 16 * CG && yo < Ho && xo < Wo;
+        const v4i v = ok ? *reinterpret_cast<const v4i*>(codes_w + lane * 16) : v4i{0, 0, 0, 0};
+        int8_t* ob = reinterpret_cast<int8_t*>(out) + (int64_t)b * Ho * Wo * ldo;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(ob, (short)0, Ho * Wo * ldo, 0x00020000);
+        const int off = ok ? (yo * Wo + xo) * ldo + 16 * cc : (int)0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, off, 0, 0);
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
+  }
+
   for (int64_t t = tw.lo + tw.slot; t < tw.hi; t += tw.team) {
     const int tx0 = (int)(t % tiles_x) * TS;
     const int ty0 = (int)((t / tiles_x) % tiles_y) * TS;
@@ -613,32 +729,7 @@ __global__ __launch_bounds__(256, CIN == 32 ? UC_MINB32 : CIN == 16 ? UC_MINB16 
     __syncthreads();
 
     v4i acc[4][G::NCT];
-#pragma unroll
-    for (int pt = 0; pt < 4; ++pt)
-#pragma unroll
-      for (int ct = 0; ct < G::NCT; ++ct) acc[pt][ct] = v4i{0, 0, 0, 0};
-#pragma unroll
-    for (int j = 0; j < G::KPAD / 64; ++j) {
-      const int kk = 64 * j + 16 * g;
-      const int tap = kk / CIN, c0 = kk % CIN;
-      const bool kv = tap < KS * KS;
-      const int kty = kv ? tap / KS : 0, ktx = kv ? tap % KS : 0;
-      v4i a[G::NCT], bf[4];
-#pragma unroll
-      for (int ct = 0; ct < G::NCT; ++ct) a[ct] = *reinterpret_cast<const v4i*>(wl + (16 * ct + p) * G::WSTR + kk);
-#pragma unroll
-      for (int pt = 0; pt < 4; ++pt) {
-        const int hy = 4 * wave + py + kty, hx = 4 * pt + px + ktx;
-        bf[pt] = *reinterpret_cast<const v4i*>(halo + (hy * G::HT + hx) * CIN + c0);
-        if (!kv) bf[pt] = v4i{0, 0, 0, 0};
-      }
-#pragma unroll
-      for (int pt = 0; pt < 4; ++pt)
-#pragma unroll
-        for (int ct = 0; ct < G::NCT; ++ct)
-          acc[pt][ct] = SW ? __builtin_amdgcn_mfma_i32_16x16x64_i8(bf[pt], a[ct], acc[pt][ct], 0, 0, 0)
-                           : __builtin_amdgcn_mfma_i32_16x16x64_i8(a[ct], bf[pt], acc[pt][ct], 0, 0, 0);
-    }
+    conv_tile(halo, acc);
 
     if constexpr (SW) {
       // acc[pt][ct][j] = conv[b][cout 16 ct + p][pool window g of patch pt, position j]
@@ -768,8 +859,22 @@ int launch_conv(const int8_t* in, int B, int H, int W, const int8_t* w, int kpad
   if (kpad < G::KPAD) return QVIT_EINVAL;
   const int64_t ntiles = (int64_t)B * ((H + TS - 1) / TS) * ((W + TS - 1) / TS);
   const int grid = (int)(ntiles < 256 * 8 ? ntiles : 256 * 8);
-  hipLaunchKernelGGL((ultra_conv_kernel<CIN, KS, COUT, POOL, OUT>), dim3(grid), dim3(256), 0, stream, in, B, H, W,
-                     w, kpad, den, alpha, shift, levels, cout_real, out, ldo, sbits);
+  // the staged pooled path: whole 16-B output groups (cout == COUT, 16-B rows) and an image of codes that a
+  // 32-bit buffer offset reaches
+  // (CIN 64: two halo buffers and the weights leave room for one workgroup per CU; that layer keeps the
+  // synchronous halo at two workgroups)
+  const bool stg = CIN <= 32 && POOL != 0 && OUT != 1 && cout_real == COUT && (ldo % 16) == 0 &&
+                   (((uintptr_t)out) & 15) == 0 &&
+                   (int64_t)(H / 2) * (W / 2) * ldo < ((int64_t)1 << 31);
+  if constexpr (CIN <= 32 && POOL != 0 && OUT != 1) {
+    if (stg) {
+      hipLaunchKernelGGL((ultra_conv_kernel<CIN, KS, COUT, POOL, OUT, true>), dim3(grid), dim3(256), 0, stream, in, B,
+                         H, W, w, kpad, den, alpha, shift, levels, cout_real, out, ldo, sbits);
+      return qvit_hip_status(hipGetLastError());
+    }
+  }
+    hipLaunchKernelGGL((ultra_conv_kernel<CIN, KS, COUT, POOL, OUT, false>), dim3(grid), dim3(256), 0, stream, in, B,
+                       H, W, w, kpad, den, alpha, shift, levels, cout_real, out, ldo, sbits);
   return qvit_hip_status(hipGetLastError());
 }
 
