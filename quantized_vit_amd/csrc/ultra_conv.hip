@@ -27,8 +27,6 @@
 //   yolo_decode               : YOLOLayer eval decode (mymodel.py:47-60) from the head's NHWC output.
 #include "qvit_common.h"
 
-#include <type_traits>
-
 namespace {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -110,7 +108,6 @@ static_assert(C0_QUADS <= 256, "one quad per thread");
 typedef _Float16 c0h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 c0h4 __attribute__((ext_vector_type(4)));
 typedef float c0f4 __attribute__((ext_vector_type(4)));
-typedef int c0i4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 QVIT_DEV float fmax_nn(float a, float b) { return __builtin_elementwise_maximum(a, b); }
@@ -197,30 +194,22 @@ __global__ __launch_bounds__(256, C0_OCC) void ultra_conv0_mfma_kernel(const flo
     const int row = t / tiles_x;
     return TPos{row / tiles_y, row - (row / tiles_y) * tiles_y, t - row * tiles_x};
   };
-  // this thread's halo quad (hy, 4 qx .. 4 qx + 3) of a tile -> registers (zero outside the image); two register
-  // sets, so the halo of tile k + 2 loads while tile k computes and tile k + 1 waits in the other set
+  // this thread's halo quad (hy, 4 qx .. 4 qx + 3) of tile t -> registers (zero outside the image)
   const int qy = tid / (C0_HX / 4), qx = tid - qy * (C0_HX / 4);
-  c0f4 xa[3], xb[3];
-  // VEC (W % 4 == 0, 12 H W < 2^31): buffer loads issued from inline asm, branch-free (a quad outside the image
-  // or a tile past the walk reads zeros: offset or record count out of range), so the compiler inserts no wait
-  // for them and the staging waits with an exact count for the one set it stages (c0_wait)
-  auto load_tile = [&](c0f4 (&xin)[3], const TPos& p, bool valid) __attribute__((always_inline)) {
+  c0f4 xin[3];
+  auto load_tile = [&](const TPos& p) __attribute__((always_inline)) {
+    if (tid >= C0_QUADS) return;
     const int b = p.b, ty0 = p.ty * C0_TY, tx0 = p.tx * C0_TX;
+    const float* base = img + (int64_t)b * 3 * HW;
     const int y = ty0 - 1 + qy, x = tx0 - 4 + 4 * qx;
-    if (VEC) {
-      const uint64_t a = reinterpret_cast<uint64_t>(img + (int64_t)b * 3 * HW);
-      const c0i4 rs = c0i4{(int)(uint32_t)a, (int)((uint32_t)(a >> 32) & 0xffff), valid ? (int)(12 * HW) : 0,
-                           0x00020000};
-      const bool ok = tid < C0_QUADS && y >= 0 && y < H && x >= 0 && x < W;
-      const int o0 = ok ? (int)(((int64_t)y * W + x) * 4) : (int)0x80000000u;
-      const int step = ok ? (int)(HW * 4) : 0;
-      asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(xin[0]) : "v"(o0), "s"(rs) : "memory");
-      asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(xin[1]) : "v"(o0 + step), "s"(rs) : "memory");
-      asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(xin[2]) : "v"(o0 + 2 * step), "s"(rs) : "memory");
+    const bool row = y >= 0 && y < H;
+    if (VEC) {  // W % 4 == 0: a quad is wholly inside or outside the row
+      const bool ok = row && x >= 0 && x < W;
+      const int64_t off = ok ? (int64_t)y * W + x : 0;
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        xin[c] = ok ? *reinterpret_cast<const c0f4*>(base + c * HW + off) : c0f4{0.f, 0.f, 0.f, 0.f};
     } else {
-      if (tid >= C0_QUADS || !valid) return;
-      const float* base = img + (int64_t)b * 3 * HW;
-      const bool row = y >= 0 && y < H;
 #pragma unroll
       for (int c = 0; c < 3; ++c)
 #pragma unroll
@@ -230,15 +219,7 @@ __global__ __launch_bounds__(256, C0_OCC) void ultra_conv0_mfma_kernel(const flo
         }
     }
   };
-  // the halo set xin has landed; N = vector-memory operations issued after its three loads (the asm loads are
-  // invisible to the compiler's wait counting, so the registers pass through the wait)
-  auto c0_wait = [&](c0f4 (&xin)[3], auto n) __attribute__((always_inline)) {
-    if (VEC) {
-      constexpr int N = decltype(n)::value;
-      asm volatile("s_waitcnt vmcnt(%3)" : "+v"(xin[0]), "+v"(xin[1]), "+v"(xin[2]) : "n"(N) : "memory");
-    }
-  };
-  auto stage_tile = [&](const c0f4 (&xin)[3], int8_t* buf) __attribute__((always_inline)) {
+  auto stage_tile = [&](int8_t* buf) __attribute__((always_inline)) {
     if (tid >= C0_QUADS) return;
     c0h8 hi[2], lo[2];
 #pragma unroll
@@ -271,16 +252,12 @@ __global__ __launch_bounds__(256, C0_OCC) void ultra_conv0_mfma_kernel(const flo
     p.b += step.b;
     return p;
   };
-  load_tile(xa, cur, true);
-  c0_wait(xa, std::integral_constant<int, 0>());
-  stage_tile(xa, smem[0]);
+  load_tile(cur);
+  stage_tile(smem[0]);
   __syncthreads();
-  TPos nxt = advance(cur);
-  int tn = t + tw.team;
-  load_tile(xb, nxt, tn < tw.hi);
   // the wave's pooled codes of a tile (2 rows x 16 columns x 16 channels) leave as 16-B pixels, 16 lanes per
   // 256-B output row; the wave reads back only what it wrote (its LDS operations complete in order). Issued
-  // after the next halo loads: a store ahead of them would make their issue wait for its completion.
+  // after the next tile's halo loads: a store ahead of them would make their issue wait for its completion.
   auto flush = [&](int b, int ty0, int tx0) __attribute__((always_inline)) {
     __builtin_amdgcn_wave_barrier();
     if (lane < 32) {
@@ -291,15 +268,15 @@ __global__ __launch_bounds__(256, C0_OCC) void ultra_conv0_mfma_kernel(const flo
     __builtin_amdgcn_wave_barrier();
   };
   int pb = 0, pty = 0, ptx = 0;  // the previous tile, its codes still in codes_l
-  // one tile: tile it computes from LDS buffer it & 1, tile it + 1 waits in xnext, tile it + 2 loads into xfree
-  auto tile_step = [&](c0f4 (&xnext)[3], c0f4 (&xfree)[3], int it) __attribute__((always_inline)) {
+  for (int it = 0; t < tw.hi; t += tw.team, ++it) {
     const int8_t* buf = smem[it & 1];
-    const int t2 = tn + tw.team;
-    const TPos nn = advance(nxt);
-    load_tile(xfree, nn, t2 < tw.hi);
-    if (it > 0) flush(pb, pty, ptx);  // (younger than the loads: the staging's count then over-waits by one)
-    const int ty0 = cur.ty * C0_TY, tx0 = cur.tx * C0_TX;
-    pb = cur.b, pty = ty0, ptx = tx0;
+    const int tn = t + tw.team;
+    const TPos nxt = advance(cur);
+    if (tn < tw.hi) load_tile(nxt);  // lands while this tile computes
+    if (it > 0) flush(pb, pty, ptx);
+    const int b = cur.b, ty0 = cur.ty * C0_TY, tx0 = cur.tx * C0_TX;
+    pb = b, pty = ty0, ptx = tx0;
+    cur = nxt;
     // A fragment records (halo pixel of tap (ky, kx): row 4 wave + py + ky, column px + kx + 3, + 4 per patch):
     // chunk 0 records r0, r1 of group g; chunk 1 = tap (2, 2) hi, then its lo (g = 0) or hi again
     auto rec = [&](int ky, int kx) { return buf + ((4 * wave + py + ky) * C0_HX + px + kx + 3) * 8; };
@@ -345,21 +322,10 @@ __global__ __launch_bounds__(256, C0_OCC) void ultra_conv0_mfma_kernel(const flo
       // one patch at a time (without the fence the scheduler hoists later patches' fragment reads: spills)
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (tn < tw.hi) {  // the other buffer: its last reader finished a barrier ago
-      c0_wait(xnext, std::integral_constant<int, 3>());  // tile it + 2's three loads may stay in flight
-      stage_tile(xnext, smem[(it + 1) & 1]);
-    }
+    if (tn < tw.hi) stage_tile(smem[(it + 1) & 1]);  // the other buffer: its last reader finished a barrier ago
     __syncthreads();
-    t = tn, tn = t2, cur = nxt, nxt = nn;
-  };
-  for (int it = 0;; it += 2) {  // two tiles per trip: the register sets swap roles
-    tile_step(xb, xa, it);
-    if (t >= tw.hi) break;
-    tile_step(xa, xb, it + 1);
-    if (t >= tw.hi) break;
   }
   flush(pb, pty, ptx);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (empty) halo loads drained before the wave ends
 }
 
 // ---- integer deploy (quantization.py:24-31,68-89; ultranet_param_gen.py) --------------------------------
@@ -917,7 +883,7 @@ extern "C" int qvit_ultra_conv0(const float* img, int64_t B, int64_t H, int64_t 
   const int64_t ntiles = B * ((H + C0_TY - 1) / C0_TY) * ((W + C0_TX - 1) / C0_TX);
   if (ntiles > INT32_MAX) return QVIT_EINVAL;
   const float levels = (float)((1 << a_bit) - 1);
-  if ((W % 4) == 0 && (((uintptr_t)img) & 15) == 0 && 12 * H * W < ((int64_t)1 << 31)) {  // 16-B buffer quad loads
+  if ((W % 4) == 0 && (((uintptr_t)img) & 15) == 0) {  // 16-B quad loads
     const int64_t grid = resident_grid(ultra_conv0_mfma_kernel<true>, ntiles);
     hipLaunchKernelGGL(ultra_conv0_mfma_kernel<true>, dim3((unsigned)grid), dim3(256), 0, stream, img, (int)B, (int)H,
                        (int)W, wvals, alpha, shift, levels, out);
