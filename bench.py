@@ -487,7 +487,11 @@ def ultranet_work(size: int = 416) -> dict:
         in_b = hw * cin * (4 if name == "ultra_conv0" else 1)
         work[name] = {"ops": 2.0 * hw * cout * cin * 9, "bytes": in_b + out_hw * cout}
     g = (size // 16) ** 2
-    work["ultra_head"] = {"ops": 2.0 * g * 36 * 64, "bytes": g * 64 + g * 36 * 4 + 2 * 2 * g * 36 * 4}
+    work["ultra_head"] = {"ops": 2.0 * g * 36 * 64, "bytes": g * 64 + g * 36 * 4}
+    work["ultra_decode"] = {"ops": 0.0, "bytes": g * 36 * 4 + 2 * g * 36 * 4}   # head in, io and p out
+    # qvit_ultra_tail (layers.16-28 in one launch, maps in LDS): layer 4's codes in, the head's fp32 out
+    work["ultra_tail"] = {"ops": sum(work[f"ultra_conv{k}"]["ops"] for k in range(4, 8)) + work["ultra_head"]["ops"],
+                          "bytes": g * 64 + g * 36 * 4}
     return work
 
 
@@ -504,7 +508,7 @@ def ultranet_main(args, world: int, rank: int, dev, backend: str, one_device: bo
     assert model.fused_ok(x)
     sharded = ShardedInference(lambda im: model(im)[0].flatten(1))
     global_batch = world * B
-    names = [n for n, *_ in ULTRA_LAYERS] + ["ultra_head"]
+    names = [n for n, *_ in ULTRA_LAYERS] + ["ultra_head", "ultra_tail", "ultra_decode"]
     with torch.no_grad():
         for _ in range(args.warmup):
             out = sharded.forward_shard(x, global_batch)
@@ -541,8 +545,9 @@ def ultranet_main(args, world: int, rank: int, dev, backend: str, one_device: bo
         kernels[n] = {"launch_us": ms * 1e3, "hbm_GBs_algorithmic": w["bytes"] * B / (ms * 1e-3) / 1e9,
                       "int8_TOPS": w["ops"] * B / (ms * 1e-3) / 1e12}
     k0 = kernels["ultra_conv0"]
-    img_bytes = sum(w["bytes"] for w in work.values())
-    img_ops = sum(w["ops"] for w in work.values())
+    per_layer = [n for n, *_ in ULTRA_LAYERS] + ["ultra_head", "ultra_decode"]   # (the tail fuses 4..7 + head)
+    img_bytes = sum(work[n]["bytes"] for n in per_layer)
+    img_ops = sum(work[n]["ops"] for n in per_layer)
     value = global_batch * args.steps / elapsed
     result = {
         "metric": f"images/sec UltraNet int4 @{size} batch {B}; % HBM roofline",

@@ -28,7 +28,8 @@
  *                             (Conv2d_Q.forward): the same contraction as an implicit GEMM over the NCHW input
  *                             (patches gathered in the kernel), NCHW fp32 out — F.conv2d(x, quantize_weight(W), b).
  *   qvit_ultra_*              4-bit quantization/quant_ultra.py:8-91 + mymodel.py:62-144 (UltraNet: weight
- *                             codes, BN folding, fused conv+BN+quantizer+maxpool blocks, YOLO decode).
+ *                             codes, BN folding, fused conv+BN+quantizer+maxpool blocks, the 26 x 26 tail of
+ *                             the network in one launch, YOLO decode).
  *   qvit_attention            vit_model.py:133-149 (Attention.forward between qkv and proj):
  *                             softmax(q k^T * scale) v per (image, head), fp32 out or fused with the
  *                             proj layer's quantize_act (quant_layers.py:497) -> int8 codes.
@@ -318,6 +319,21 @@ int qvit_ultra_conv0(const float* img, int64_t B, int64_t H, int64_t W, const fl
 int qvit_ultra_conv(const int8_t* in, int64_t B, int64_t H, int64_t W, int64_t cin, int64_t ks,
                     const int8_t* wcodes, int64_t kpad, int64_t cout, int w_bit, int a_bit,
                     const float* alpha, const float* shift, int mode, void* out, int64_t ldo,
+                    hipStream_t stream);
+/*
+ * qvit_ultra_tail: UltraNetQua.layers.16-28 (mymodel.py:104-124: four Conv2d_Q 64 -> 64 3x3 + BatchNorm2d +
+ *   activation_quantize_fn blocks, then the 1x1 Conv2d_Q head with bias) in one launch, one workgroup per image
+ *   with the maps resident in LDS. Same results as qvit_ultra_conv(QVIT_ULTRA_CODES) four times and
+ *   qvit_ultra_conv(QVIT_ULTRA_F32) once, bit for bit.
+ *   in      : codes NHWC [B][H][W][64], H, W <= 26 (UltraNet @416: 26 x 26), 16-byte aligned.
+ *   wcodes, alpha, shift : HOST arrays of 4 device pointers (layers 4..7): weight codes [64][kpad] in K order
+ *             (ky, kx, c) (qvit_ultra_weight_codes, kpad >= 576, % 16), BN alpha / shift [64] (qvit_ultra_bn_fold).
+ *   hcodes  : head codes [48][hkpad] (hkpad >= 64); hbias device float[hout], hout <= 48.
+ *   out     : fp32 NHWC [B][H][W][ldo], channels < hout written.
+ */
+int qvit_ultra_tail(const int8_t* in, int64_t B, int64_t H, int64_t W, const int8_t* const* wcodes, int64_t kpad,
+                    const float* const* alpha, const float* const* shift, const int8_t* hcodes, int64_t hkpad,
+                    const float* hbias, int64_t hout, int w_bit, int a_bit, float* out, int64_t ldo,
                     hipStream_t stream);
 /*
  * UltraNet integer deploy (reference `4-bit quantization/`: quantization.py:24-31,68-89,

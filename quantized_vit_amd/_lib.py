@@ -76,6 +76,8 @@ _SIGNATURES = {
     "qvit_ultra_conv0": [_c_p, _i64, _i64, _i64, _c_p, _c_p, _c_p, _i32, _c_p, _c_p],
     "qvit_ultra_conv": [_c_p, _i64, _i64, _i64, _i64, _i64, _c_p, _i64, _i64, _i32, _i32, _c_p, _c_p, _i32, _c_p,
                         _i64, _c_p],
+    "qvit_ultra_tail": [_c_p, _i64, _i64, _i64, _c_p, _i64, _c_p, _c_p, _c_p, _i64, _c_p, _i64, _i32, _i32, _c_p,
+                        _i64, _c_p],
     "qvit_ultra_conv0_int": [_c_p, _i64, _i64, _i64, _c_p, _c_p, _c_p, _i32, _i32, _c_p, _c_p],
     "qvit_ultra_conv_int": [_c_p, _i64, _i64, _i64, _i64, _i64, _c_p, _i64, _i64, _c_p, _c_p, _i32, _i32, _i32,
                             _c_p, _i64, _c_p],
@@ -468,6 +470,21 @@ def ultra_conv(x: torch.Tensor, ks: int, wcodes: torch.Tensor, cout: int, w_bit:
     _check(load().qvit_ultra_conv(_ptr(x), B, H, W, cin, ks, _ptr(wcodes), wcodes.shape[1], cout, w_bit, a_bit,
                                   _ptr(alpha), _ptr(shift), mode, _ptr(out), cout, _stream(x.device)),
            "qvit_ultra_conv")
+    return out
+
+
+def ultra_tail(x: torch.Tensor, wcodes, alphas, shifts, hcodes: torch.Tensor, hbias: torch.Tensor, hout: int,
+               w_bit: int, a_bit: int) -> torch.Tensor:
+    """UltraNet layers.16-28 in one launch (qvit_ultra_tail): NHWC codes [B][H][W][64] (H, W <= 26) through four
+    3x3 64 -> 64 blocks and the 1x1 head -> fp32 NHWC [B][H][W][hout]."""
+    _require_gpu(x, "codes")
+    assert x.dtype == torch.int8 and x.is_contiguous() and x.shape[3] == 64
+    B, H, W, _ = x.shape
+    out = torch.empty((B, H, W, hout), dtype=torch.float32, device=x.device)
+    arr = lambda ts: (ctypes.c_void_p * 4)(*[t.data_ptr() for t in ts])
+    _check(load().qvit_ultra_tail(_ptr(x), B, H, W, arr(wcodes), wcodes[0].shape[1], arr(alphas), arr(shifts),
+                                  _ptr(hcodes), hcodes.shape[1], _ptr(hbias), hout, w_bit, a_bit, _ptr(out), hout,
+                                  _stream(x.device)), "qvit_ultra_tail")
     return out
 
 

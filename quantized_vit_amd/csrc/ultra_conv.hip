@@ -766,6 +766,139 @@ __global__ __launch_bounds__(256, STG ? 2 : CIN == 32 ? UC_MINB32 : CIN == 16 ? 
   }
 }
 
+// ---- layers.16-28 in one launch: conv4 .. conv7 (64 -> 64, 3x3, BN + quantizer) and the 1x1 head ---------------
+// At 416 x 416 these five layers run on 26 x 26 maps: per image 43 KB of codes in and out of each layer, so as
+// separate launches they are latency-bound (≈ 28 µs each for ≈ 2.5 µs of MFMA work at b256). Here one workgroup
+// (8 waves) owns one image: its codes stay in LDS through all five layers, in two zero-bordered [H + 2][W + 2][64]
+// images used in turn (the border is the 3x3 conv's zero padding), and each layer's weight codes are staged in
+// LDS before it runs. The arithmetic is ultra_conv_kernel's (A = weights, B = 16 pixels of a 4 x 4 patch, exact
+// int32 accumulation, the same BN + quantizer and head epilogues), so the outputs are bit-identical to the
+// per-layer launches. Maps up to 26 x 26 (LDS: 2 x 49 KiB images + 38 KiB of weights).
+constexpr int TL_MAX = 26;
+constexpr int TL_IMG = (TL_MAX + 2) * (TL_MAX + 2) * 64;  // 50 176 B
+constexpr int TL_WSTR = 9 * 64 + 32;                       // 3x3 weight row pitch (conflict-free b128 reads)
+constexpr int TL_HSTR = 64 + 32;                           // head weight row pitch
+struct TailArgs {
+  const int8_t* w[4];
+  const float* alpha[4];
+  const float* shift[4];
+};
+
+__global__ __launch_bounds__(512, 1) void ultra_tail_kernel(const int8_t* __restrict__ in, int H, int W, TailArgs ta,
+                                                            int kpad, const int8_t* __restrict__ hw, int hkpad,
+                                                            const float* __restrict__ hbias, int hout, float den,
+                                                            float levels, float* __restrict__ out, int ldo) {
+  __shared__ __attribute__((aligned(16))) int8_t smem[2 * TL_IMG + 64 * TL_WSTR];
+  int8_t* imgA = smem;
+  int8_t* imgB = smem + TL_IMG;
+  int8_t* wl = smem + 2 * TL_IMG;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int p = lane & 15, g = lane >> 4;
+  const int b = blockIdx.x;
+  const int WP = W + 2;
+  const int PX = (W + 3) / 4, NP = ((H + 3) / 4) * PX;
+
+  // zero both images (borders), then the input codes into A's interior
+  for (int i = tid; i < 2 * TL_IMG / 16; i += 512) reinterpret_cast<v4i*>(smem)[i] = v4i{0, 0, 0, 0};
+  __syncthreads();
+  for (int i = tid; i < H * W * 4; i += 512) {
+    const int pix = i >> 2, c16 = i & 3, y = pix / W, x = pix - (pix / W) * W;
+    *reinterpret_cast<v4i*>(imgA + ((y + 1) * WP + x + 1) * 64 + 16 * c16) =
+        *reinterpret_cast<const v4i*>(in + ((int64_t)b * H * W + pix) * 64 + 16 * c16);
+  }
+  auto load_w = [&](const int8_t* w, int rows, int kbytes, int kp, int stride) __attribute__((always_inline)) {
+    const int per = kbytes / 16;
+    for (int i = tid; i < rows * per; i += 512) {
+      const int o = i / per, c16 = i - o * per;
+      *reinterpret_cast<v4i*>(wl + o * stride + 16 * c16) = *reinterpret_cast<const v4i*>(w + (int64_t)o * kp + 16 * c16);
+    }
+  };
+  load_w(ta.w[0], 64, 9 * 64, kpad, TL_WSTR);
+  __syncthreads();
+
+  for (int l = 0; l < 4; ++l) {
+    const int8_t* src = (l & 1) ? imgB : imgA;
+    int8_t* dst = (l & 1) ? imgA : imgB;
+    float al[4][4], sh[4][4];
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        al[ct][j] = ta.alpha[l][16 * ct + 4 * g + j];
+        sh[ct][j] = ta.shift[l][16 * ct + 4 * g + j];
+      }
+    // patches P = wave + 8 i, two at a time (one weight fragment read feeds both)
+    for (int pi = wave; pi < NP; pi += 16) {
+      const int pq[2] = {pi, pi + 8};
+      v4i acc[2][4];
+      int py[2], px[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int P = pq[q] < NP ? pq[q] : pi;
+        py[q] = 4 * (P / PX) + (p >> 2);
+        px[q] = 4 * (P - (P / PX) * PX) + (p & 3);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) acc[q][ct] = v4i{0, 0, 0, 0};
+      }
+#pragma unroll
+      for (int j = 0; j < 9; ++j) {  // tap j = (ky, kx); lane group g: channels 16 g .. 16 g + 15
+        const int ky = j / 3, kx = j - 3 * (j / 3);
+        v4i a[4];
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) a[ct] = *reinterpret_cast<const v4i*>(wl + (16 * ct + p) * TL_WSTR + 64 * j + 16 * g);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          // pixels past the map (the last patches' overhang) read a valid pixel and are never stored
+          const int y = py[q] < H ? py[q] : H - 1, x = px[q] < W ? px[q] : W - 1;
+          const v4i bf = *reinterpret_cast<const v4i*>(src + ((y + ky) * WP + x + kx) * 64 + 16 * g);
+#pragma unroll
+          for (int ct = 0; ct < 4; ++ct) acc[q][ct] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[ct], bf, acc[q][ct], 0, 0, 0);
+        }
+      }
+      // acc[q][ct][j] = conv[channel 16 ct + 4 g + j][pixel (py, px)] -> codes into dst's interior
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        if (pq[q] >= NP || py[q] >= H || px[q] >= W) continue;
+        int8_t* d = dst + ((py[q] + 1) * WP + px[q] + 1) * 64 + 4 * g;
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) {
+          uint32_t word = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            word |= (uint32_t)act_code((float)acc[q][ct][j] / den, al[ct][j], sh[ct][j], levels) << (8 * j);
+          *reinterpret_cast<uint32_t*>(d + 16 * ct) = word;
+        }
+      }
+    }
+    __syncthreads();  // every read of this layer's weights and source image done, dst complete
+    if (l < 3) load_w(ta.w[l + 1], 64, 9 * 64, kpad, TL_WSTR);
+    else load_w(hw, 48, 64, hkpad, TL_HSTR);
+    __syncthreads();
+  }
+
+  // head (1x1, 64 -> hout <= 48, bias, fp32 NHWC out) from image A (conv7's output)
+  for (int pi = wave; pi < NP; pi += 8) {
+    const int py = 4 * (pi / PX) + (p >> 2), px = 4 * (pi - (pi / PX) * PX) + (p & 3);
+    const int y = py < H ? py : H - 1, x = px < W ? px : W - 1;
+    const v4i bf = *reinterpret_cast<const v4i*>(imgA + ((y + 1) * WP + x + 1) * 64 + 16 * g);
+    v4i acc[3];
+#pragma unroll
+    for (int ct = 0; ct < 3; ++ct)
+      acc[ct] = __builtin_amdgcn_mfma_i32_16x16x64_i8(*reinterpret_cast<const v4i*>(wl + (16 * ct + p) * TL_HSTR + 16 * g), bf,
+                                                      v4i{0, 0, 0, 0}, 0, 0, 0);
+    if (py >= H || px >= W) continue;
+    float* o = out + ((int64_t)b * H * W + py * W + px) * ldo;
+#pragma unroll
+    for (int ct = 0; ct < 3; ++ct)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = 16 * ct + 4 * g + j;
+        if (c < hout) o[c] = __fadd_rn((float)acc[ct][j] / den, hbias[c]);
+      }
+  }
+}
+
 // ---- YOLOLayer decode (mymodel.py:47-60) -----------------------------------------------------------
 // (32-bit index arithmetic: the launcher checks the element count fits; 64-bit divisions cost more than the
 // decode itself)
@@ -926,6 +1059,33 @@ extern "C" int qvit_ultra_conv(const int8_t* in, int64_t B, int64_t H, int64_t W
   QVIT_ULTRA_CASE(64, 1, 48)
 #undef QVIT_ULTRA_CASE
   return QVIT_EINVAL;  // shapes outside UltraNetQua's layer set
+}
+
+extern "C" int qvit_ultra_tail(const int8_t* in, int64_t B, int64_t H, int64_t W, const int8_t* const* wcodes,
+                               int64_t kpad, const float* const* alpha, const float* const* shift,
+                               const int8_t* hcodes, int64_t hkpad, const float* hbias, int64_t hout, int w_bit,
+                               int a_bit, float* out, int64_t ldo, hipStream_t stream) {
+  if (!in || !wcodes || !alpha || !shift || !hcodes || !hbias || !out) return QVIT_ENULL;
+  for (int l = 0; l < 4; ++l)
+    if (!wcodes[l] || !alpha[l] || !shift[l]) return QVIT_ENULL;
+  if (B < 0 || H < 1 || W < 1 || H > TL_MAX || W > TL_MAX || hout < 1 || hout > 48 || ldo < hout) return QVIT_EINVAL;
+  if (kpad < 9 * 64 || hkpad < 64 || w_bit < 2 || w_bit > 8 || a_bit < 1 || a_bit > 7) return QVIT_EINVAL;
+  if (B > INT32_MAX) return QVIT_EINVAL;
+  if ((((uintptr_t)in) & 15) || (kpad % 16) || (hkpad % 16) || (((uintptr_t)hcodes) & 15)) return QVIT_EALIGN;
+  for (int l = 0; l < 4; ++l)
+    if (((uintptr_t)wcodes[l]) & 15) return QVIT_EALIGN;
+  if (B == 0) return QVIT_OK;
+  TailArgs ta;
+  for (int l = 0; l < 4; ++l) {
+    ta.w[l] = wcodes[l];
+    ta.alpha[l] = alpha[l];
+    ta.shift[l] = shift[l];
+  }
+  const float den = (float)(((1 << (w_bit - 1)) - 1) * ((1 << a_bit) - 1));
+  const float lv = (float)((1 << a_bit) - 1);
+  hipLaunchKernelGGL(ultra_tail_kernel, dim3((unsigned)B), dim3(512), 0, stream, in, (int)H, (int)W, ta, (int)kpad,
+                     hcodes, (int)hkpad, hbias, (int)hout, den, lv, out, (int)ldo);
+  return qvit_hip_status(hipGetLastError());
 }
 
 extern "C" int qvit_ultra_conv0_int(const uint8_t* img, int64_t B, int64_t H, int64_t W, const int8_t* wcodes,

@@ -2,11 +2,12 @@
 MI355X forward.
 
 Same module tree as the reference (state_dict keys layers.{i}.*, yololayer attributes), so a reference
-checkpoint loads unchanged. In eval mode on a ROCm device the network runs as 10 HIP launches:
+checkpoint loads unchanged. In eval mode on a ROCm device the network runs as 6 HIP launches at 416 x 416:
 
   layers.0-3   qvit_ultra_conv0  float image -> conv3x3 (W4) -> BN -> A4 quantizer -> maxpool -> NHWC codes
-  layers.4-27  qvit_ultra_conv   codes -> implicit-GEMM conv on MFMA -> BN -> quantizer (-> maxpool)
-  layers.28    qvit_ultra_conv   1x1 head, acc/105 + bias -> fp32
+  layers.4-15  qvit_ultra_conv   codes -> implicit-GEMM conv on MFMA -> BN -> quantizer -> maxpool
+  layers.16-28 qvit_ultra_tail   the four 26 x 26 blocks and the 1x1 head (acc/105 + bias -> fp32) in one
+                                 launch, the maps resident in LDS (qvit_ultra_conv per layer for larger maps)
   yololayer    qvit_yolo_decode
 
 Weight codes and BN constants are prepared once per parameter version (a plan cache, like the ViT
@@ -78,6 +79,7 @@ class YOLOLayer(nn.Module):
 
 W_BIT = 4
 A_BIT = 4
+TAIL_MAX = 26  # qvit_ultra_tail: maps up to 26 x 26 (416 x 416 images) stay in LDS
 
 
 def _conv_stack(w_bit=W_BIT, a_bit=A_BIT):
@@ -180,11 +182,20 @@ class UltraNetQua(nn.Module):
         with _timed("ultra_conv0"):
             h = _lib.ultra_conv0(x.contiguous(), c0, a0, s0, A_BIT)
         for k, (codes, alpha, shift, cout, pool) in enumerate(plan[1:], 1):
+            if k == 4 and h.shape[1] <= TAIL_MAX and h.shape[2] <= TAIL_MAX:
+                # layers.16-28 (the four unpooled blocks and the head) in one launch, maps resident in LDS
+                tail = plan[4:]
+                with _timed("ultra_tail"):
+                    head = _lib.ultra_tail(h, [c for c, *_ in tail], [a for _, a, *_ in tail],
+                                           [s for _, _, s, *_ in tail], hcodes, hbias, hout, W_BIT, A_BIT)
+                break
             mode = _lib.ULTRA_CODES_POOL if pool else _lib.ULTRA_CODES
             with _timed(f"ultra_conv{k}"):
                 h = _lib.ultra_conv(h, 3, codes, cout, W_BIT, A_BIT, alpha, shift, mode)
-        with _timed("ultra_head"):
-            head = _lib.ultra_conv(h, 1, hcodes, hout, W_BIT, A_BIT, None, hbias, _lib.ULTRA_F32)
+        else:
+            with _timed("ultra_head"):
+                head = _lib.ultra_conv(h, 1, hcodes, hout, W_BIT, A_BIT, None, hbias, _lib.ULTRA_F32)
+        with _timed("ultra_decode"):
             io, p = self.yololayer.decode_nhwc(head, img_size)
         return io, (p,)   # = torch.cat((io,), 1): the single YOLO layer's output, already a fresh tensor
 

@@ -228,3 +228,50 @@ def test_production_schedule_b256(dev):
     for got, want, want64 in ((gio[sel], io, io64), (gp[0][sel], p, p64)):
         floor = rel(want64, want)
         assert rel(got, want) <= max(1e-3, 2.5 * floor), (rel(got, want), floor)
+
+
+@pytest.mark.parametrize("size", [(416, 416), (208, 320), (64, 48)])
+def test_tail_kernel_equals_per_layer_launches(dev, size):
+    """qvit_ultra_tail (layers.16-28 in one launch, maps in LDS) against the per-layer qvit_ultra_conv launches it
+    replaces: the same integer accumulations and epilogues, so io and p are bit-identical; square and non-square
+    maps, including overhanging 4 x 4 patches (13 x 20, 4 x 3)."""
+    import quantized_vit_amd.ultranet as un
+    model = random_ultranet(seed=5, device=dev, calib_batch=1, img_size=max(size))
+    g = torch.Generator().manual_seed(sum(size))
+    img = (torch.randint(0, 256, (3, 3) + size, generator=g).float() / 255.0).to(dev)
+    assert model.fused_ok(img)
+    with torch.no_grad():
+        io_t, p_t = model.forward_fused(img)
+        saved = un.TAIL_MAX
+        un.TAIL_MAX = 0
+        try:
+            io_l, p_l = model.forward_fused(img)
+        finally:
+            un.TAIL_MAX = saved
+    assert torch.equal(p_t[0], p_l[0])
+    assert torch.equal(io_t, io_l)
+
+
+def test_tail_argument_validation(dev):
+    lib = _lib.load()
+    import ctypes
+    s = torch.cuda.current_stream().cuda_stream
+    x = torch.zeros(1, 26, 26, 64, dtype=torch.int8, device=dev)
+    w = torch.zeros(64, 576, dtype=torch.int8, device=dev)
+    a = torch.zeros(64, device=dev)
+    hw = torch.zeros(48, 64, dtype=torch.int8, device=dev)
+    out = torch.empty(1, 26, 26, 36, device=dev)
+    ws = (ctypes.c_void_p * 4)(*[w.data_ptr()] * 4)
+    al = (ctypes.c_void_p * 4)(*[a.data_ptr()] * 4)
+
+    def call(H=26, W=26, kpad=576, hout=36, ldo=36, wb=4):
+        return lib.qvit_ultra_tail(x.data_ptr(), 1, H, W, ws, kpad, al, al, hw.data_ptr(), 64, a.data_ptr(), hout,
+                                   wb, 4, out.data_ptr(), ldo, s)
+    assert call() == 0
+    assert call(H=27) != 0          # map larger than the LDS images
+    assert call(kpad=512) != 0      # fewer than 9 x 64 weight columns
+    assert call(hout=49) != 0
+    assert call(ldo=30) != 0
+    assert call(wb=9) != 0
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
