@@ -773,9 +773,12 @@ __global__ __launch_bounds__(256, STG ? 2 : CIN == 32 ? UC_MINB32 : CIN == 16 ? 
 // images used in turn (the border is the 3x3 conv's zero padding), and each layer's weight codes are staged in
 // LDS before it runs. The arithmetic is ultra_conv_kernel's (A = weights, B = 16 pixels of a 4 x 4 patch, exact
 // int32 accumulation, the same BN + quantizer and head epilogues), so the outputs are bit-identical to the
-// per-layer launches. Maps up to 26 x 26 (LDS: 2 x 49 KiB images + 38 KiB of weights).
+// per-layer launches. Maps up to 26 x 26 (LDS: 2 x 50 KiB images + 38 KiB of weights).
 constexpr int TL_MAX = 26;
-constexpr int TL_IMG = (TL_MAX + 2) * (TL_MAX + 2) * 64;  // 50 176 B
+// image rows of (W + 2) pixels x 64 B plus 32 B: a row pitch of 8 (mod 16) dwords puts the 16 pixels of a 4 x 4
+// patch read by one ds_read_b128 lane group on distinct banks (a multiple of 64 dwords gave 2-way conflicts)
+constexpr int TL_RPAD = 32;
+constexpr int TL_IMG = (TL_MAX + 2) * ((TL_MAX + 2) * 64 + TL_RPAD);  // 51 072 B
 constexpr int TL_WSTR = 9 * 64 + 32;                       // 3x3 weight row pitch (conflict-free b128 reads)
 constexpr int TL_HSTR = 64 + 32;                           // head weight row pitch
 struct TailArgs {
@@ -796,7 +799,7 @@ __global__ __launch_bounds__(512, 1) void ultra_tail_kernel(const int8_t* __rest
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int p = lane & 15, g = lane >> 4;
   const int b = blockIdx.x;
-  const int WP = W + 2;
+  const int RP = (W + 2) * 64 + TL_RPAD;  // image row pitch (bytes)
   const int PX = (W + 3) / 4, NP = ((H + 3) / 4) * PX;
 
   // zero both images (borders), then the input codes into A's interior
@@ -804,17 +807,35 @@ __global__ __launch_bounds__(512, 1) void ultra_tail_kernel(const int8_t* __rest
   __syncthreads();
   for (int i = tid; i < H * W * 4; i += 512) {
     const int pix = i >> 2, c16 = i & 3, y = pix / W, x = pix - (pix / W) * W;
-    *reinterpret_cast<v4i*>(imgA + ((y + 1) * WP + x + 1) * 64 + 16 * c16) =
+    *reinterpret_cast<v4i*>(imgA + (y + 1) * RP + (x + 1) * 64 + 16 * c16) =
         *reinterpret_cast<const v4i*>(in + ((int64_t)b * H * W + pix) * 64 + 16 * c16);
   }
-  auto load_w = [&](const int8_t* w, int rows, int kbytes, int kp, int stride) __attribute__((always_inline)) {
+  // a layer's weight codes pass through registers: the next layer's are loaded while the current one computes
+  // (64 x 576 B = 4.5 16-B pieces per thread), and written to LDS once every wave is done with the current ones
+  constexpr int WPT = (64 * 36 + 511) / 512;
+  v4i wpre[WPT];
+  auto fetch_w = [&](const int8_t* w, int rows, int kbytes, int kp) __attribute__((always_inline)) {
     const int per = kbytes / 16;
-    for (int i = tid; i < rows * per; i += 512) {
-      const int o = i / per, c16 = i - o * per;
-      *reinterpret_cast<v4i*>(wl + o * stride + 16 * c16) = *reinterpret_cast<const v4i*>(w + (int64_t)o * kp + 16 * c16);
+#pragma unroll
+    for (int k = 0; k < WPT; ++k) {
+      const int i = tid + 512 * k, o = i / per, c16 = i - o * per;
+      // (issued from asm: the compiler would drain an ordinary load before the patch loop that it outlives)
+      const int8_t* src = w + (int64_t)(i < rows * per ? o : 0) * kp + 16 * (i < rows * per ? c16 : 0);
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(wpre[k]) : "v"(src) : "memory");
     }
   };
-  load_w(ta.w[0], 64, 9 * 64, kpad, TL_WSTR);
+  auto put_w = [&](int rows, int kbytes, int stride) __attribute__((always_inline)) {
+    const int per = kbytes / 16;
+    static_assert(WPT == 5, "the wait's operand list");
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(wpre[0]), "+v"(wpre[1]), "+v"(wpre[2]), "+v"(wpre[3]), "+v"(wpre[4])::"memory");
+#pragma unroll
+    for (int k = 0; k < WPT; ++k) {
+      const int i = tid + 512 * k, o = i / per, c16 = i - o * per;
+      if (i < rows * per) *reinterpret_cast<v4i*>(wl + o * stride + 16 * c16) = wpre[k];
+    }
+  };
+  fetch_w(ta.w[0], 64, 9 * 64, kpad);
+  put_w(64, 9 * 64, TL_WSTR);
   __syncthreads();
 
   for (int l = 0; l < 4; ++l) {
@@ -828,6 +849,14 @@ __global__ __launch_bounds__(512, 1) void ultra_tail_kernel(const int8_t* __rest
         al[ct][j] = ta.alpha[l][16 * ct + 4 * g + j];
         sh[ct][j] = ta.shift[l][16 * ct + 4 * g + j];
       }
+    // (the BN constants arrive first: a use inside the patch loop of a value still loading makes the compiler
+    // drain every load before the loop, the weight prefetch included)
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+      asm volatile("" ::"v"(al[ct][0]), "v"(al[ct][1]), "v"(al[ct][2]), "v"(al[ct][3]), "v"(sh[ct][0]), "v"(sh[ct][1]),
+                   "v"(sh[ct][2]), "v"(sh[ct][3]));
+    if (l < 3) fetch_w(ta.w[l + 1], 64, 9 * 64, kpad);  // lands while this layer computes
+    else fetch_w(hw, 48, 64, hkpad);
     // patches P = wave + 8 i, two at a time (one weight fragment read feeds both)
     for (int pi = wave; pi < NP; pi += 16) {
       const int pq[2] = {pi, pi + 8};
@@ -851,7 +880,7 @@ __global__ __launch_bounds__(512, 1) void ultra_tail_kernel(const int8_t* __rest
         for (int q = 0; q < 2; ++q) {
           // pixels past the map (the last patches' overhang) read a valid pixel and are never stored
           const int y = py[q] < H ? py[q] : H - 1, x = px[q] < W ? px[q] : W - 1;
-          const v4i bf = *reinterpret_cast<const v4i*>(src + ((y + ky) * WP + x + kx) * 64 + 16 * g);
+          const v4i bf = *reinterpret_cast<const v4i*>(src + (y + ky) * RP + (x + kx) * 64 + 16 * g);
 #pragma unroll
           for (int ct = 0; ct < 4; ++ct) acc[q][ct] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[ct], bf, acc[q][ct], 0, 0, 0);
         }
@@ -860,7 +889,7 @@ __global__ __launch_bounds__(512, 1) void ultra_tail_kernel(const int8_t* __rest
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         if (pq[q] >= NP || py[q] >= H || px[q] >= W) continue;
-        int8_t* d = dst + ((py[q] + 1) * WP + px[q] + 1) * 64 + 4 * g;
+        int8_t* d = dst + (py[q] + 1) * RP + (px[q] + 1) * 64 + 4 * g;
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct) {
           uint32_t word = 0;
@@ -872,8 +901,8 @@ __global__ __launch_bounds__(512, 1) void ultra_tail_kernel(const int8_t* __rest
       }
     }
     __syncthreads();  // every read of this layer's weights and source image done, dst complete
-    if (l < 3) load_w(ta.w[l + 1], 64, 9 * 64, kpad, TL_WSTR);
-    else load_w(hw, 48, 64, hkpad, TL_HSTR);
+    if (l < 3) put_w(64, 9 * 64, TL_WSTR);
+    else put_w(48, 64, TL_HSTR);
     __syncthreads();
   }
 
@@ -881,7 +910,7 @@ __global__ __launch_bounds__(512, 1) void ultra_tail_kernel(const int8_t* __rest
   for (int pi = wave; pi < NP; pi += 8) {
     const int py = 4 * (pi / PX) + (p >> 2), px = 4 * (pi - (pi / PX) * PX) + (p & 3);
     const int y = py < H ? py : H - 1, x = px < W ? px : W - 1;
-    const v4i bf = *reinterpret_cast<const v4i*>(imgA + ((y + 1) * WP + x + 1) * 64 + 16 * g);
+    const v4i bf = *reinterpret_cast<const v4i*>(imgA + (y + 1) * RP + (x + 1) * 64 + 16 * g);
     v4i acc[3];
 #pragma unroll
     for (int ct = 0; ct < 3; ++ct)
