@@ -781,6 +781,7 @@ constexpr int TL_RPAD = 32;
 constexpr int TL_IMG = (TL_MAX + 2) * ((TL_MAX + 2) * 64 + TL_RPAD);  // 51 072 B
 constexpr int TL_WSTR = 9 * 64 + 32;                       // 3x3 weight row pitch (conflict-free b128 reads)
 constexpr int TL_HSTR = 64 + 32;                           // head weight row pitch
+constexpr int TL_PW = ((TL_MAX + 3) / 4) * ((TL_MAX + 3) / 4) / 8 + 1;  // 4 x 4 patches per wave (7 at 26 x 26)
 struct TailArgs {
   const int8_t* w[4];
   const float* alpha[4];
@@ -792,6 +793,7 @@ __global__ __launch_bounds__(512, 1) void ultra_tail_kernel(const int8_t* __rest
                                                             const float* __restrict__ hbias, int hout, float den,
                                                             float levels, float* __restrict__ out, int ldo) {
   __shared__ __attribute__((aligned(16))) int8_t smem[2 * TL_IMG + 64 * TL_WSTR];
+  __shared__ __attribute__((aligned(16))) float bn_l[4][2][64];  // every layer's BN alpha / shift
   int8_t* imgA = smem;
   int8_t* imgB = smem + TL_IMG;
   int8_t* wl = smem + 2 * TL_IMG;
@@ -834,6 +836,11 @@ __global__ __launch_bounds__(512, 1) void ultra_tail_kernel(const int8_t* __rest
       if (i < rows * per) *reinterpret_cast<v4i*>(wl + o * stride + 16 * c16) = wpre[k];
     }
   };
+  if (tid < 4 * 64) {
+    const int l = tid >> 6, c = tid & 63;
+    bn_l[l][0][c] = ta.alpha[l][c];
+    bn_l[l][1][c] = ta.shift[l][c];
+  }
   fetch_w(ta.w[0], 64, 9 * 64, kpad);
   put_w(64, 9 * 64, TL_WSTR);
   __syncthreads();
@@ -841,63 +848,54 @@ __global__ __launch_bounds__(512, 1) void ultra_tail_kernel(const int8_t* __rest
   for (int l = 0; l < 4; ++l) {
     const int8_t* src = (l & 1) ? imgB : imgA;
     int8_t* dst = (l & 1) ? imgA : imgB;
-    float al[4][4], sh[4][4];
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        al[ct][j] = ta.alpha[l][16 * ct + 4 * g + j];
-        sh[ct][j] = ta.shift[l][16 * ct + 4 * g + j];
-      }
-    // (the BN constants arrive first: a use inside the patch loop of a value still loading makes the compiler
-    // drain every load before the loop, the weight prefetch included)
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct)
-      asm volatile("" ::"v"(al[ct][0]), "v"(al[ct][1]), "v"(al[ct][2]), "v"(al[ct][3]), "v"(sh[ct][0]), "v"(sh[ct][1]),
-                   "v"(sh[ct][2]), "v"(sh[ct][3]));
     if (l < 3) fetch_w(ta.w[l + 1], 64, 9 * 64, kpad);  // lands while this layer computes
     else fetch_w(hw, 48, 64, hkpad);
-    // patches P = wave + 8 i, two at a time (one weight fragment read feeds both)
-    for (int pi = wave; pi < NP; pi += 16) {
-      const int pq[2] = {pi, pi + 8};
-      v4i acc[2][4];
-      int py[2], px[2];
+    // the wave's patches P = wave + 8 k (k < TL_PW) all at once: each weight fragment read feeds TL_PW patches
+    v4i acc[TL_PW][4];
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int P = pq[q] < NP ? pq[q] : pi;
-        py[q] = 4 * (P / PX) + (p >> 2);
-        px[q] = 4 * (P - (P / PX) * PX) + (p & 3);
+    for (int k = 0; k < TL_PW; ++k)
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) acc[q][ct] = v4i{0, 0, 0, 0};
+      for (int ct = 0; ct < 4; ++ct) acc[k][ct] = v4i{0, 0, 0, 0};
+    // pixel of this lane in patch k (recomputed where used: arrays of them would stay live across the taps)
+    auto pix = [&](int k, int& py, int& px) __attribute__((always_inline)) {
+      const int P = wave + 8 * k < NP ? wave + 8 * k : wave;
+      py = 4 * (P / PX) + (p >> 2);
+      px = 4 * (P - (P / PX) * PX) + (p & 3);
+    };
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {  // tap j = (ky, kx); lane group g: channels 16 g .. 16 g + 15
+      const int ky = j / 3, kx = j - 3 * (j / 3);
+      v4i a[4];
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) a[ct] = *reinterpret_cast<const v4i*>(wl + (16 * ct + p) * TL_WSTR + 64 * j + 16 * g);
+#pragma unroll
+      for (int k = 0; k < TL_PW; ++k) {
+        if (wave + 8 * k >= NP) continue;  // wave-uniform
+        // pixels past the map (the last patches' overhang) read a valid pixel and are never stored
+        int py, px;
+        pix(k, py, px);
+        const int y = py < H ? py : H - 1, x = px < W ? px : W - 1;
+        const v4i bf = *reinterpret_cast<const v4i*>(src + (y + ky) * RP + (x + kx) * 64 + 16 * g);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) acc[k][ct] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[ct], bf, acc[k][ct], 0, 0, 0);
       }
+    }
+    // acc[k][ct][j] = conv[channel 16 ct + 4 g + j][pixel (py, px)] -> codes into dst's interior
 #pragma unroll
-      for (int j = 0; j < 9; ++j) {  // tap j = (ky, kx); lane group g: channels 16 g .. 16 g + 15
-        const int ky = j / 3, kx = j - 3 * (j / 3);
-        v4i a[4];
+    for (int k = 0; k < TL_PW; ++k) {
+      int py, px;
+      pix(k, py, px);
+      if (wave + 8 * k >= NP || py >= H || px >= W) continue;
+      int8_t* d = dst + (py + 1) * RP + (px + 1) * 64 + 4 * g;
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) a[ct] = *reinterpret_cast<const v4i*>(wl + (16 * ct + p) * TL_WSTR + 64 * j + 16 * g);
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          // pixels past the map (the last patches' overhang) read a valid pixel and are never stored
-          const int y = py[q] < H ? py[q] : H - 1, x = px[q] < W ? px[q] : W - 1;
-          const v4i bf = *reinterpret_cast<const v4i*>(src + (y + ky) * RP + (x + kx) * 64 + 16 * g);
-#pragma unroll
-          for (int ct = 0; ct < 4; ++ct) acc[q][ct] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[ct], bf, acc[q][ct], 0, 0, 0);
-        }
-      }
-      // acc[q][ct][j] = conv[channel 16 ct + 4 g + j][pixel (py, px)] -> codes into dst's interior
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        if (pq[q] >= NP || py[q] >= H || px[q] >= W) continue;
-        int8_t* d = dst + (py[q] + 1) * RP + (px[q] + 1) * 64 + 4 * g;
-#pragma unroll
-        for (int ct = 0; ct < 4; ++ct) {
-          uint32_t word = 0;
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            word |= (uint32_t)act_code((float)acc[q][ct][j] / den, al[ct][j], sh[ct][j], levels) << (8 * j);
-          *reinterpret_cast<uint32_t*>(d + 16 * ct) = word;
-        }
+      for (int ct = 0; ct < 4; ++ct) {
+        const float4 al = *reinterpret_cast<const float4*>(&bn_l[l][0][16 * ct + 4 * g]);
+        const float4 sh = *reinterpret_cast<const float4*>(&bn_l[l][1][16 * ct + 4 * g]);
+        const uint32_t word = (uint32_t)act_code((float)acc[k][ct][0] / den, al.x, sh.x, levels) |
+                              ((uint32_t)act_code((float)acc[k][ct][1] / den, al.y, sh.y, levels) << 8) |
+                              ((uint32_t)act_code((float)acc[k][ct][2] / den, al.z, sh.z, levels) << 16) |
+                              ((uint32_t)act_code((float)acc[k][ct][3] / den, al.w, sh.w, levels) << 24);
+        *reinterpret_cast<uint32_t*>(d + 16 * ct) = word;
       }
     }
     __syncthreads();  // every read of this layer's weights and source image done, dst complete
