@@ -329,11 +329,14 @@ int qvit_ultra_conv(const int8_t* in, int64_t B, int64_t H, int64_t W, int64_t c
  *   wcodes, alpha, shift : HOST arrays of 4 device pointers (layers 4..7): weight codes [64][kpad] in K order
  *             (ky, kx, c) (qvit_ultra_weight_codes, kpad >= 576, % 16), BN alpha / shift [64] (qvit_ultra_bn_fold).
  *   hcodes  : head codes [48][hkpad] (hkpad >= 64); hbias device float[hout], hout <= 48.
- *   out     : fp32 NHWC [B][H][W][ldo], channels < hout written.
+ *   out     : fp32 NHWC [B][H][W][ldo], channels < hout written (io == NULL), or
+ *   anchors, na, no, stride, io, p : with io != NULL the YOLOLayer decode of qvit_yolo_decode is applied in the
+ *             kernel instead (hout == na * no; io, p [B][na][H][W][no]; out unused and may be NULL).
  */
 int qvit_ultra_tail(const int8_t* in, int64_t B, int64_t H, int64_t W, const int8_t* const* wcodes, int64_t kpad,
                     const float* const* alpha, const float* const* shift, const int8_t* hcodes, int64_t hkpad,
                     const float* hbias, int64_t hout, int w_bit, int a_bit, float* out, int64_t ldo,
+                    const float* anchors, int64_t na, int64_t no, float stride, float* io, float* p,
                     hipStream_t stream);
 /*
  * UltraNet integer deploy (reference `4-bit quantization/`: quantization.py:24-31,68-89,

@@ -77,7 +77,7 @@ _SIGNATURES = {
     "qvit_ultra_conv": [_c_p, _i64, _i64, _i64, _i64, _i64, _c_p, _i64, _i64, _i32, _i32, _c_p, _c_p, _i32, _c_p,
                         _i64, _c_p],
     "qvit_ultra_tail": [_c_p, _i64, _i64, _i64, _c_p, _i64, _c_p, _c_p, _c_p, _i64, _c_p, _i64, _i32, _i32, _c_p,
-                        _i64, _c_p],
+                        _i64, _c_p, _i64, _i64, _f32, _c_p, _c_p, _c_p],
     "qvit_ultra_conv0_int": [_c_p, _i64, _i64, _i64, _c_p, _c_p, _c_p, _i32, _i32, _c_p, _c_p],
     "qvit_ultra_conv_int": [_c_p, _i64, _i64, _i64, _i64, _i64, _c_p, _i64, _i64, _c_p, _c_p, _i32, _i32, _i32,
                             _c_p, _i64, _c_p],
@@ -474,18 +474,29 @@ def ultra_conv(x: torch.Tensor, ks: int, wcodes: torch.Tensor, cout: int, w_bit:
 
 
 def ultra_tail(x: torch.Tensor, wcodes, alphas, shifts, hcodes: torch.Tensor, hbias: torch.Tensor, hout: int,
-               w_bit: int, a_bit: int) -> torch.Tensor:
+               w_bit: int, a_bit: int, decode=None):
     """UltraNet layers.16-28 in one launch (qvit_ultra_tail): NHWC codes [B][H][W][64] (H, W <= 26) through four
-    3x3 64 -> 64 blocks and the 1x1 head -> fp32 NHWC [B][H][W][hout]."""
+    3x3 64 -> 64 blocks and the 1x1 head -> fp32 NHWC [B][H][W][hout]; with decode = (anchors, na, no, stride)
+    the YOLO decode runs in the kernel and (io [B, na*H*W, no], p [B, na, H, W, no]) is returned instead."""
     _require_gpu(x, "codes")
     assert x.dtype == torch.int8 and x.is_contiguous() and x.shape[3] == 64
     B, H, W, _ = x.shape
-    out = torch.empty((B, H, W, hout), dtype=torch.float32, device=x.device)
     arr = lambda ts: (ctypes.c_void_p * 4)(*[t.data_ptr() for t in ts])
+    if decode is None:
+        out = torch.empty((B, H, W, hout), dtype=torch.float32, device=x.device)
+        io = p = anchors = None
+        na = no = 0
+        stride = 0.0
+    else:
+        anchors, na, no, stride = decode
+        out = None
+        io = torch.empty((B, na, H, W, no), device=x.device)
+        p = torch.empty_like(io)
     _check(load().qvit_ultra_tail(_ptr(x), B, H, W, arr(wcodes), wcodes[0].shape[1], arr(alphas), arr(shifts),
                                   _ptr(hcodes), hcodes.shape[1], _ptr(hbias), hout, w_bit, a_bit, _ptr(out), hout,
-                                  _stream(x.device)), "qvit_ultra_tail")
-    return out
+                                  _ptr(anchors), na, no, float(stride), _ptr(io), _ptr(p), _stream(x.device)),
+           "qvit_ultra_tail")
+    return out if decode is None else (io.view(B, -1, no), p)
 
 
 def ultra_conv0_int(img_u8: torch.Tensor, wcodes: torch.Tensor, inc: torch.Tensor, bias: torch.Tensor,

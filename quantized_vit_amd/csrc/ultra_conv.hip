@@ -766,6 +766,13 @@ __global__ __launch_bounds__(256, STG ? 2 : CIN == 32 ? UC_MINB32 : CIN == 16 ? 
   }
 }
 
+// YOLOLayer eval decode of one head value v = p[..][o] of anchor a at grid cell (x, y) (mymodel.py:56-59)
+QVIT_DEV float yolo_io(float v, int o, int a, int x, int y, const float* __restrict__ anchors, float stride) {
+  if (o < 2) return __fmul_rn(__fadd_rn(1.f / (1.f + expf(-v)), (float)(o == 0 ? x : y)), stride);
+  if (o < 4) return __fmul_rn(__fmul_rn(expf(v), anchors[2 * a + (o - 2)] / stride), stride);  // anchor_vec = anchors / stride
+  return 1.f / (1.f + expf(-v));
+}
+
 // ---- layers.16-28 in one launch: conv4 .. conv7 (64 -> 64, 3x3, BN + quantizer) and the 1x1 head ---------------
 // At 416 x 416 these five layers run on 26 x 26 maps: per image 43 KB of codes in and out of each layer, so as
 // separate launches they are latency-bound (≈ 28 µs each for ≈ 2.5 µs of MFMA work at b256). Here one workgroup
@@ -788,10 +795,20 @@ struct TailArgs {
   const float* shift[4];
 };
 
+// DEC: the YOLO decode of the head output (qvit_yolo_decode's arithmetic) into io / p instead of the fp32 head
+struct TailDecode {
+  const float* anchors;
+  int na, no;
+  float stride;
+  float* io;
+  float* p;
+};
+template <bool DEC>
 __global__ __launch_bounds__(512, 1) void ultra_tail_kernel(const int8_t* __restrict__ in, int H, int W, TailArgs ta,
                                                             int kpad, const int8_t* __restrict__ hw, int hkpad,
                                                             const float* __restrict__ hbias, int hout, float den,
-                                                            float levels, float* __restrict__ out, int ldo) {
+                                                            float levels, float* __restrict__ out, int ldo,
+                                                            TailDecode dec) {
   __shared__ __attribute__((aligned(16))) int8_t smem[2 * TL_IMG + 64 * TL_WSTR];
   __shared__ __attribute__((aligned(16))) float bn_l[4][2][64];  // every layer's BN alpha / shift
   int8_t* imgA = smem;
@@ -921,7 +938,16 @@ __global__ __launch_bounds__(512, 1) void ultra_tail_kernel(const int8_t* __rest
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int c = 16 * ct + 4 * g + j;
-        if (c < hout) o[c] = __fadd_rn((float)acc[ct][j] / den, hbias[c]);
+        if (c >= hout) continue;
+        const float v = __fadd_rn((float)acc[ct][j] / den, hbias[c]);
+        if (DEC) {  // p[b][a][y][x][o] = head channel a no + o, io its decode
+          const int a = c / dec.no, oo = c - a * dec.no;
+          const int64_t i = ((((int64_t)b * dec.na + a) * H + py) * W + px) * dec.no + oo;
+          dec.p[i] = v;
+          dec.io[i] = yolo_io(v, oo, a, px, py, dec.anchors, dec.stride);
+        } else {
+          o[c] = v;
+        }
       }
   }
 }
@@ -946,17 +972,7 @@ __global__ void yolo_decode_kernel(const float* __restrict__ head, int B, int ny
     // p[b][a][y][x][o] = head_nchw[b][a*no + o][y][x] = head_nhwc[b][y][x][a*no + o]
     const float v = head[(((int64_t)b * ny + y) * nx + x) * ldh + a * no + o];
     pout[i] = v;
-    float r;
-    if (o < 2) {
-      r = __fadd_rn(1.f / (1.f + expf(-v)), (float)(o == 0 ? x : y));
-      r = __fmul_rn(r, stride);
-    } else if (o < 4) {
-      const float awh = anchors[2 * a + (o - 2)] / stride;  // anchor_vec = anchors / stride
-      r = __fmul_rn(__fmul_rn(expf(v), awh), stride);
-    } else {
-      r = 1.f / (1.f + expf(-v));
-    }
-    io[i] = r;
+    io[i] = yolo_io(v, o, a, x, y, anchors, stride);
   }
 }
 
@@ -1091,11 +1107,16 @@ extern "C" int qvit_ultra_conv(const int8_t* in, int64_t B, int64_t H, int64_t W
 extern "C" int qvit_ultra_tail(const int8_t* in, int64_t B, int64_t H, int64_t W, const int8_t* const* wcodes,
                                int64_t kpad, const float* const* alpha, const float* const* shift,
                                const int8_t* hcodes, int64_t hkpad, const float* hbias, int64_t hout, int w_bit,
-                               int a_bit, float* out, int64_t ldo, hipStream_t stream) {
-  if (!in || !wcodes || !alpha || !shift || !hcodes || !hbias || !out) return QVIT_ENULL;
+                               int a_bit, float* out, int64_t ldo, const float* anchors, int64_t na, int64_t no,
+                               float stride, float* io, float* p, hipStream_t stream) {
+  const bool dec = io != nullptr;
+  if (!in || !wcodes || !alpha || !shift || !hcodes || !hbias) return QVIT_ENULL;
+  if (dec ? (!p || !anchors) : !out) return QVIT_ENULL;
+  if (dec && (na < 1 || no < 5 || na * no != hout || !(stride > 0.f))) return QVIT_EINVAL;
   for (int l = 0; l < 4; ++l)
     if (!wcodes[l] || !alpha[l] || !shift[l]) return QVIT_ENULL;
-  if (B < 0 || H < 1 || W < 1 || H > TL_MAX || W > TL_MAX || hout < 1 || hout > 48 || ldo < hout) return QVIT_EINVAL;
+  if (B < 0 || H < 1 || W < 1 || H > TL_MAX || W > TL_MAX || hout < 1 || hout > 48 || (!dec && ldo < hout))
+    return QVIT_EINVAL;
   if (kpad < 9 * 64 || hkpad < 64 || w_bit < 2 || w_bit > 8 || a_bit < 1 || a_bit > 7) return QVIT_EINVAL;
   if (B > INT32_MAX) return QVIT_EINVAL;
   if ((((uintptr_t)in) & 15) || (kpad % 16) || (hkpad % 16) || (((uintptr_t)hcodes) & 15)) return QVIT_EALIGN;
@@ -1110,8 +1131,13 @@ extern "C" int qvit_ultra_tail(const int8_t* in, int64_t B, int64_t H, int64_t W
   }
   const float den = (float)(((1 << (w_bit - 1)) - 1) * ((1 << a_bit) - 1));
   const float lv = (float)((1 << a_bit) - 1);
-  hipLaunchKernelGGL(ultra_tail_kernel, dim3((unsigned)B), dim3(512), 0, stream, in, (int)H, (int)W, ta, (int)kpad,
-                     hcodes, (int)hkpad, hbias, (int)hout, den, lv, out, (int)ldo);
+  const TailDecode td{anchors, (int)na, (int)no, stride, io, p};
+  if (dec)
+    hipLaunchKernelGGL(ultra_tail_kernel<true>, dim3((unsigned)B), dim3(512), 0, stream, in, (int)H, (int)W, ta,
+                       (int)kpad, hcodes, (int)hkpad, hbias, (int)hout, den, lv, out, (int)ldo, td);
+  else
+    hipLaunchKernelGGL(ultra_tail_kernel<false>, dim3((unsigned)B), dim3(512), 0, stream, in, (int)H, (int)W, ta,
+                       (int)kpad, hcodes, (int)hkpad, hbias, (int)hout, den, lv, out, (int)ldo, td);
   return qvit_hip_status(hipGetLastError());
 }
 

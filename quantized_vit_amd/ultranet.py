@@ -2,13 +2,13 @@
 MI355X forward.
 
 Same module tree as the reference (state_dict keys layers.{i}.*, yololayer attributes), so a reference
-checkpoint loads unchanged. In eval mode on a ROCm device the network runs as 6 HIP launches at 416 x 416:
+checkpoint loads unchanged. In eval mode on a ROCm device the network runs as 5 HIP launches at 416 x 416:
 
   layers.0-3   qvit_ultra_conv0  float image -> conv3x3 (W4) -> BN -> A4 quantizer -> maxpool -> NHWC codes
   layers.4-15  qvit_ultra_conv   codes -> implicit-GEMM conv on MFMA -> BN -> quantizer -> maxpool
-  layers.16-28 qvit_ultra_tail   the four 26 x 26 blocks and the 1x1 head (acc/105 + bias -> fp32) in one
-                                 launch, the maps resident in LDS (qvit_ultra_conv per layer for larger maps)
-  yololayer    qvit_yolo_decode
+  layers.16-28 qvit_ultra_tail   the four 26 x 26 blocks, the 1x1 head (acc/105 + bias) and the YOLO decode
+  + yololayer                    in one launch, the maps resident in LDS (for larger maps: qvit_ultra_conv per
+                                 layer, then qvit_yolo_decode)
 
 Weight codes and BN constants are prepared once per parameter version (a plan cache, like the ViT
 layers). Anything else (training mode, CPU tensors, non-reference layer stacks) runs module by module.
@@ -65,16 +65,21 @@ class YOLOLayer(nn.Module):
         torch.sigmoid_(io[..., 4:])
         return io.view(bs, -1, self.no), p
 
+    def decode_params(self, ny: int, nx: int, img_size, device):
+        """(anchors on the device, na, no, stride) of the decode at an ny x nx grid (create_grids, mymodel.py:7-21)."""
+        if (self.nx, self.ny) != (nx, ny):
+            create_grids(self, img_size, (nx, ny), device, torch.float32)
+        dev_anchors = getattr(self, "_dev_anchors", None)
+        if dev_anchors is None or dev_anchors.device != device:
+            dev_anchors = self.anchors.to(device, torch.float32).contiguous()
+            self._dev_anchors = dev_anchors
+        return dev_anchors, self.na, self.no, float(self.stride)
+
     def decode_nhwc(self, head: torch.Tensor, img_size):
         """The same decode on the device from the head conv's NHWC output (qvit_yolo_decode)."""
         bs, ny, nx, _ = head.shape
-        if (self.nx, self.ny) != (nx, ny):
-            create_grids(self, img_size, (nx, ny), head.device, head.dtype)
-        dev_anchors = getattr(self, "_dev_anchors", None)
-        if dev_anchors is None or dev_anchors.device != head.device:
-            dev_anchors = self.anchors.to(head.device, torch.float32).contiguous()
-            self._dev_anchors = dev_anchors
-        return _lib.yolo_decode(head, self.na, self.no, dev_anchors, float(self.stride))
+        anchors, na, no, stride = self.decode_params(ny, nx, img_size, head.device)
+        return _lib.yolo_decode(head, na, no, anchors, stride)
 
 
 W_BIT = 4
@@ -182,13 +187,15 @@ class UltraNetQua(nn.Module):
         with _timed("ultra_conv0"):
             h = _lib.ultra_conv0(x.contiguous(), c0, a0, s0, A_BIT)
         for k, (codes, alpha, shift, cout, pool) in enumerate(plan[1:], 1):
-            if k == 4 and h.shape[1] <= TAIL_MAX and h.shape[2] <= TAIL_MAX:
-                # layers.16-28 (the four unpooled blocks and the head) in one launch, maps resident in LDS
+            if k == 4 and h.shape[1] <= TAIL_MAX and h.shape[2] <= TAIL_MAX and hout == self.yololayer.na * 6:
+                # layers.16-28 (the four unpooled blocks and the head) and the YOLO decode in one launch, the maps
+                # resident in LDS
                 tail = plan[4:]
+                dec = self.yololayer.decode_params(h.shape[1], h.shape[2], img_size, h.device)
                 with _timed("ultra_tail"):
-                    head = _lib.ultra_tail(h, [c for c, *_ in tail], [a for _, a, *_ in tail],
-                                           [s for _, _, s, *_ in tail], hcodes, hbias, hout, W_BIT, A_BIT)
-                break
+                    io, p = _lib.ultra_tail(h, [c for c, *_ in tail], [a for _, a, *_ in tail],
+                                            [s for _, _, s, *_ in tail], hcodes, hbias, hout, W_BIT, A_BIT, decode=dec)
+                return io, (p,)
             mode = _lib.ULTRA_CODES_POOL if pool else _lib.ULTRA_CODES
             with _timed(f"ultra_conv{k}"):
                 h = _lib.ultra_conv(h, 3, codes, cout, W_BIT, A_BIT, alpha, shift, mode)

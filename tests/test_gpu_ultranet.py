@@ -232,9 +232,10 @@ def test_production_schedule_b256(dev):
 
 @pytest.mark.parametrize("size", [(416, 416), (208, 320), (64, 48)])
 def test_tail_kernel_equals_per_layer_launches(dev, size):
-    """qvit_ultra_tail (layers.16-28 in one launch, maps in LDS) against the per-layer qvit_ultra_conv launches it
-    replaces: the same integer accumulations and epilogues, so io and p are bit-identical; square and non-square
-    maps, including overhanging 4 x 4 patches (13 x 20, 4 x 3)."""
+    """qvit_ultra_tail (layers.16-28 and the YOLO decode in one launch, maps in LDS) against the per-layer
+    qvit_ultra_conv launches and qvit_yolo_decode it replaces: the same integer accumulations, epilogues and decode
+    arithmetic, so io and p are bit-identical; square and non-square maps, including overhanging 4 x 4 patches
+    (13 x 20, 4 x 3)."""
     import quantized_vit_amd.ultranet as un
     model = random_ultranet(seed=5, device=dev, calib_batch=1, img_size=max(size))
     g = torch.Generator().manual_seed(sum(size))
@@ -264,14 +265,22 @@ def test_tail_argument_validation(dev):
     ws = (ctypes.c_void_p * 4)(*[w.data_ptr()] * 4)
     al = (ctypes.c_void_p * 4)(*[a.data_ptr()] * 4)
 
-    def call(H=26, W=26, kpad=576, hout=36, ldo=36, wb=4):
+    anchors = torch.full((6, 2), 20.0, device=dev)
+    io = torch.empty(1, 6, 26, 26, 6, device=dev)
+    pp = torch.empty_like(io)
+
+    def call(H=26, W=26, kpad=576, hout=36, ldo=36, wb=4, dec=False, na=6, stride=16.0):
         return lib.qvit_ultra_tail(x.data_ptr(), 1, H, W, ws, kpad, al, al, hw.data_ptr(), 64, a.data_ptr(), hout,
-                                   wb, 4, out.data_ptr(), ldo, s)
+                                   wb, 4, None if dec else out.data_ptr(), ldo, anchors.data_ptr(), na, 6, stride,
+                                   io.data_ptr() if dec else None, pp.data_ptr() if dec else None, s)
     assert call() == 0
+    assert call(dec=True) == 0
     assert call(H=27) != 0          # map larger than the LDS images
     assert call(kpad=512) != 0      # fewer than 9 x 64 weight columns
     assert call(hout=49) != 0
     assert call(ldo=30) != 0
     assert call(wb=9) != 0
+    assert call(dec=True, na=5) != 0      # na * no != hout
+    assert call(dec=True, stride=0.0) != 0
     torch.cuda.synchronize()
-    assert torch.isfinite(out).all()
+    assert torch.isfinite(out).all() and torch.isfinite(io).all()
