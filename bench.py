@@ -489,9 +489,9 @@ def ultranet_work(size: int = 416) -> dict:
     g = (size // 16) ** 2
     work["ultra_head"] = {"ops": 2.0 * g * 36 * 64, "bytes": g * 64 + g * 36 * 4}
     work["ultra_decode"] = {"ops": 0.0, "bytes": g * 36 * 4 + 2 * g * 36 * 4}   # head in, io and p out
-    # qvit_ultra_tail (layers.16-28 in one launch, maps in LDS): layer 4's codes in, the head's fp32 out
+    # qvit_ultra_tail (layers.16-28 + the YOLO decode in one launch, maps in LDS): layer 4's codes in, io and p out
     work["ultra_tail"] = {"ops": sum(work[f"ultra_conv{k}"]["ops"] for k in range(4, 8)) + work["ultra_head"]["ops"],
-                          "bytes": g * 64 + g * 36 * 4}
+                          "bytes": g * 64 + 2 * g * 36 * 4}
     return work
 
 
