@@ -820,14 +820,26 @@ __global__ __launch_bounds__(512, 1) void ultra_tail_kernel(const int8_t* __rest
   const int b = blockIdx.x;
   const int RP = (W + 2) * 64 + TL_RPAD;  // image row pitch (bytes)
   const int PX = (W + 3) / 4, NP = ((H + 3) / 4) * PX;
+  // P / PX as a multiply-shift (exact for P < 64, PX <= 7: the fractional parts of P / PX stay below 6 / 7)
+  const int pinv = (65536 + PX - 1) / PX;
+  auto pdiv = [&](int P) __attribute__((always_inline)) { return (P * pinv) >> 16; };
 
   // zero both images (borders), then the input codes into A's interior
   for (int i = tid; i < 2 * TL_IMG / 16; i += 512) reinterpret_cast<v4i*>(smem)[i] = v4i{0, 0, 0, 0};
   __syncthreads();
-  for (int i = tid; i < H * W * 4; i += 512) {
-    const int pix = i >> 2, c16 = i & 3, y = pix / W, x = pix - (pix / W) * W;
-    *reinterpret_cast<v4i*>(imgA + (y + 1) * RP + (x + 1) * 64 + 16 * c16) =
-        *reinterpret_cast<const v4i*>(in + ((int64_t)b * H * W + pix) * 64 + 16 * c16);
+  {  // all of a thread's input pieces in flight at once (a rolled loop waited for each in turn)
+    constexpr int IPT = (TL_MAX * TL_MAX * 4 + 511) / 512;
+    v4i v[IPT];
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const int i = tid + 512 * k;
+      if (i < H * W * 4) v[k] = *reinterpret_cast<const v4i*>(in + (int64_t)b * H * W * 64 + 16 * i);
+    }
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const int i = tid + 512 * k, pix = i >> 2, c16 = i & 3, y = pix / W, x = pix - (pix / W) * W;
+      if (i < H * W * 4) *reinterpret_cast<v4i*>(imgA + (y + 1) * RP + (x + 1) * 64 + 16 * c16) = v[k];
+    }
   }
   // a layer's weight codes pass through registers: the next layer's are loaded while the current one computes
   // (64 x 576 B = 4.5 16-B pieces per thread), and written to LDS once every wave is done with the current ones
@@ -876,8 +888,9 @@ __global__ __launch_bounds__(512, 1) void ultra_tail_kernel(const int8_t* __rest
     // pixel of this lane in patch k (recomputed where used: arrays of them would stay live across the taps)
     auto pix = [&](int k, int& py, int& px) __attribute__((always_inline)) {
       const int P = wave + 8 * k < NP ? wave + 8 * k : wave;
-      py = 4 * (P / PX) + (p >> 2);
-      px = 4 * (P - (P / PX) * PX) + (p & 3);
+      const int pr = pdiv(P);
+      py = 4 * pr + (p >> 2);
+      px = 4 * (P - pr * PX) + (p & 3);
     };
 #pragma unroll
     for (int j = 0; j < 9; ++j) {  // tap j = (ky, kx); lane group g: channels 16 g .. 16 g + 15
@@ -923,7 +936,8 @@ __global__ __launch_bounds__(512, 1) void ultra_tail_kernel(const int8_t* __rest
 
   // head (1x1, 64 -> hout <= 48, bias, fp32 NHWC out) from image A (conv7's output)
   for (int pi = wave; pi < NP; pi += 8) {
-    const int py = 4 * (pi / PX) + (p >> 2), px = 4 * (pi - (pi / PX) * PX) + (p & 3);
+    const int pr = pdiv(pi);
+    const int py = 4 * pr + (p >> 2), px = 4 * (pi - pr * PX) + (p & 3);
     const int y = py < H ? py : H - 1, x = px < W ? px : W - 1;
     const v4i bf = *reinterpret_cast<const v4i*>(imgA + (y + 1) * RP + (x + 1) * 64 + 16 * g);
     v4i acc[3];
