@@ -71,6 +71,15 @@ __global__ void ultra_bn_fold_kernel(const float* gamma, const float* beta, cons
   shift[c] = __fsub_rn(beta ? beta[c] : 0.f, __fmul_rn(mean[c], a));
 }
 
+// acc / den for an integer accumulator |acc| < 2^24 and the small integer den = (2^(w-1) - 1)(2^a - 1): the
+// reciprocal product with one exact FMA residual correction (3 VALU instead of the IEEE divide's ~10); the
+// per-layer kernels and the fused tail use the same form, so their codes agree bit for bit
+QVIT_DEV float acc_div(int acc, float den, float rden) {
+  const float x = (float)acc;
+  const float q0 = x * rden;
+  return fmaf(fmaf(-q0, den, x), rden, q0);
+}
+
 QVIT_DEV int act_code(float x, float alpha, float shift, float levels) {
   const float y = __fadd_rn(__fmul_rn(x, alpha), shift);
   return (int)rintf(fminf(fmaxf(y, 0.f), 1.f) * levels);
@@ -522,6 +531,7 @@ __global__ __launch_bounds__(256, STG ? 2 : CIN == 32 ? UC_MINB32 : CIN == 16 ? 
                                                             int cout_real, void* __restrict__ out, int ldo,
                                                             int sbits) {
   using G = ConvGeo<CIN, KS, COUT>;
+  const float rden = 1.f / den;
   constexpr bool STAGED = STG && POOL != 0 && OUT != 1;
   constexpr int HALO16 = (G::HALO + 15) / 16 * 16;
   constexpr int WOUT = 2 * (TS / 2) * COUT;  // a wave's pooled codes per tile (2 rows x 8 columns)
@@ -658,7 +668,7 @@ __global__ __launch_bounds__(256, STG ? 2 : CIN == 32 ? UC_MINB32 : CIN == 16 ? 
           const int vmax = max(max(v[0], v[1]), max(v[2], v[3]));
           const int vmin = min(min(v[0], v[1]), min(v[2], v[3]));
           const int code = (OUT == 2) ? int_code(iincs[ct] < 0 ? vmin : vmax, iincs[ct], ibiass[ct], sbits, (int)levels)
-                                      : act_code((float)(als[ct] < 0.f ? vmin : vmax) / den, als[ct], shs[ct], levels);
+                                      : act_code(acc_div(als[ct] < 0.f ? vmin : vmax, den, rden), als[ct], shs[ct], levels);
           cw[2 * pt * COUT + 16 * ct] = (int8_t)code;
         }
       __builtin_amdgcn_wave_barrier();
@@ -710,7 +720,7 @@ __global__ __launch_bounds__(256, STG ? 2 : CIN == 32 ? UC_MINB32 : CIN == 16 ? 
           const int vmax = max(max(v[0], v[1]), max(v[2], v[3]));
           const int vmin = min(min(v[0], v[1]), min(v[2], v[3]));
           const int code = (OUT == 2) ? int_code(iincs[ct] < 0 ? vmin : vmax, iincs[ct], ibiass[ct], sbits, (int)levels)
-                                      : act_code((float)(als[ct] < 0.f ? vmin : vmax) / den, als[ct], shs[ct], levels);
+                                      : act_code(acc_div(als[ct] < 0.f ? vmin : vmax, den, rden), als[ct], shs[ct], levels);
           const uint32_t word = pack_quad(code);  // channels 16 ct + p .. + 3 in lane p = 4k
           const int o = 16 * ct + p;
           if ((p & 3) == 0 && yo < Ho && xo < Wo && o < cout_real)
@@ -734,14 +744,14 @@ __global__ __launch_bounds__(256, STG ? 2 : CIN == 32 ? UC_MINB32 : CIN == 16 ? 
             float* dst = reinterpret_cast<float*>(out) + (((int64_t)b * H + y) * W + x) * ldo;
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-              if (o0 + j < cout_real) dst[o0 + j] = __fadd_rn((float)acc[pt][ct][j] / den, sh[ct][j]);
+              if (o0 + j < cout_real) dst[o0 + j] = __fadd_rn(acc_div(acc[pt][ct][j], den, rden), sh[ct][j]);
           }
         } else {
           int code[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             code[j] = (OUT == 2) ? int_code(acc[pt][ct][j], iinc[ct][j], ibias[ct][j], sbits, (int)levels)
-                                 : act_code((float)acc[pt][ct][j] / den, al[ct][j], sh[ct][j], levels);
+                                 : act_code(acc_div(acc[pt][ct][j], den, rden), al[ct][j], sh[ct][j], levels);
           if (POOL) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -818,6 +828,7 @@ __global__ __launch_bounds__(512, 1) void ultra_tail_kernel(const int8_t* __rest
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int p = lane & 15, g = lane >> 4;
   const int b = blockIdx.x;
+  const float rden = 1.f / den;
   const int RP = (W + 2) * 64 + TL_RPAD;  // image row pitch (bytes)
   const int PX = (W + 3) / 4, NP = ((H + 3) / 4) * PX;
   // P / PX as a multiply-shift (exact for P < 64, PX <= 7: the fractional parts of P / PX stay below 6 / 7)
@@ -921,10 +932,10 @@ __global__ __launch_bounds__(512, 1) void ultra_tail_kernel(const int8_t* __rest
       for (int ct = 0; ct < 4; ++ct) {
         const float4 al = *reinterpret_cast<const float4*>(&bn_l[l][0][16 * ct + 4 * g]);
         const float4 sh = *reinterpret_cast<const float4*>(&bn_l[l][1][16 * ct + 4 * g]);
-        const uint32_t word = (uint32_t)act_code((float)acc[k][ct][0] / den, al.x, sh.x, levels) |
-                              ((uint32_t)act_code((float)acc[k][ct][1] / den, al.y, sh.y, levels) << 8) |
-                              ((uint32_t)act_code((float)acc[k][ct][2] / den, al.z, sh.z, levels) << 16) |
-                              ((uint32_t)act_code((float)acc[k][ct][3] / den, al.w, sh.w, levels) << 24);
+        const uint32_t word = (uint32_t)act_code(acc_div(acc[k][ct][0], den, rden), al.x, sh.x, levels) |
+                              ((uint32_t)act_code(acc_div(acc[k][ct][1], den, rden), al.y, sh.y, levels) << 8) |
+                              ((uint32_t)act_code(acc_div(acc[k][ct][2], den, rden), al.z, sh.z, levels) << 16) |
+                              ((uint32_t)act_code(acc_div(acc[k][ct][3], den, rden), al.w, sh.w, levels) << 24);
         *reinterpret_cast<uint32_t*>(d + 16 * ct) = word;
       }
     }
@@ -953,7 +964,7 @@ __global__ __launch_bounds__(512, 1) void ultra_tail_kernel(const int8_t* __rest
       for (int j = 0; j < 4; ++j) {
         const int c = 16 * ct + 4 * g + j;
         if (c >= hout) continue;
-        const float v = __fadd_rn((float)acc[ct][j] / den, hbias[c]);
+        const float v = __fadd_rn(acc_div(acc[ct][j], den, rden), hbias[c]);
         if (DEC) {  // p[b][a][y][x][o] = head channel a no + o, io its decode
           const int a = c / dec.no, oo = c - a * dec.no;
           const int64_t i = ((((int64_t)b * dec.na + a) * H + py) * W + px) * dec.no + oo;
