@@ -903,6 +903,15 @@ __global__ __launch_bounds__(512, 1) void ultra_tail_kernel(const int8_t* __rest
       py = 4 * pr + (p >> 2);
       px = 4 * (P - pr * PX) + (p & 3);
     };
+    // this lane's pixel of each patch as an LDS byte offset (pixels past the map, the last patches' overhang,
+    // read a valid pixel and are never stored)
+    int poff[TL_PW];
+#pragma unroll
+    for (int k = 0; k < TL_PW; ++k) {
+      int py, px;
+      pix(k, py, px);
+      poff[k] = (py < H ? py : H - 1) * RP + (px < W ? px : W - 1) * 64 + 16 * g;
+    }
 #pragma unroll
     for (int j = 0; j < 9; ++j) {  // tap j = (ky, kx); lane group g: channels 16 g .. 16 g + 15
       const int ky = j / 3, kx = j - 3 * (j / 3);
@@ -912,11 +921,7 @@ __global__ __launch_bounds__(512, 1) void ultra_tail_kernel(const int8_t* __rest
 #pragma unroll
       for (int k = 0; k < TL_PW; ++k) {
         if (wave + 8 * k >= NP) continue;  // wave-uniform
-        // pixels past the map (the last patches' overhang) read a valid pixel and are never stored
-        int py, px;
-        pix(k, py, px);
-        const int y = py < H ? py : H - 1, x = px < W ? px : W - 1;
-        const v4i bf = *reinterpret_cast<const v4i*>(src + (y + ky) * RP + (x + kx) * 64 + 16 * g);
+        const v4i bf = *reinterpret_cast<const v4i*>(src + poff[k] + ky * RP + kx * 64);
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct) acc[k][ct] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[ct], bf, acc[k][ct], 0, 0, 0);
       }
