@@ -46,11 +46,20 @@ def pmc_values(d, counter):
 
 
 def _build_id():
-    """The profiled library's build id (quantized_vit_amd._lib.build_id; no torch import needed)."""
+    """The profiled library's build id, as quantized_vit_amd._lib.build_id computes it (the digest of its build
+    inputs that build.py writes beside it; the bytes' sha256 without one) — no torch import needed."""
     import hashlib
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "quantized_vit_amd", "libqvit_hip.so")
     try:
-        with open(os.path.join(root, "quantized_vit_amd", "libqvit_hip.so"), "rb") as f:
+        with open(lib + ".srcsha") as f:
+            digest = f.read().strip()
+        if digest:
+            return "src-" + digest[:16]
+    except OSError:
+        pass
+    try:
+        with open(lib, "rb") as f:
             return hashlib.sha256(f.read()).hexdigest()[:16]
     except OSError:
         return None
