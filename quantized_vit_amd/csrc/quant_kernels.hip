@@ -299,15 +299,9 @@ __global__ __launch_bounds__(kThreads) void layernorm_quant_reg_kernel(
 // rows wave, wave + nwaves, ... with the next row's load in flight while the current row is finished;
 // gamma/beta, the quantizer scalars and the code table (QVIT_EPI_I8 semantics, nullable) are read once
 // per workgroup. Same arithmetic as layernorm_quant_reg_kernel, row for row.
-#ifndef QVIT_LN_TBL_BYTES
-#define QVIT_LN_TBL_BYTES 16384
-#endif
-constexpr int LN_TBL_BYTES = QVIT_LN_TBL_BYTES;
-#ifndef QVIT_LN_MINW
-#define QVIT_LN_MINW 1
-#endif
+constexpr int LN_TBL_BYTES = 16384;
 template <int NV>
-__global__ __launch_bounds__(kThreads, QVIT_LN_MINW) void layernorm_quant_persist_kernel(
+__global__ __launch_bounds__(kThreads, 1) void layernorm_quant_persist_kernel(
     const float* __restrict__ x, int64_t rows, int64_t cols, int64_t ldx, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, int qtype, const float* d, const float* qm, const float* t,
     int levels, int8_t* __restrict__ codes, int64_t ldc, int64_t kpad, const int8_t* __restrict__ table) {
