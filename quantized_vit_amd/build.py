@@ -19,8 +19,8 @@ BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libqvit_hip.so")
 ARCH = "gfx950"
 
-SOURCES = ["quant_kernels.hip", "gemm_w4a8.hip", "gemm_wonly.hip", "attention.hip", "qkv_attention.hip",
-           "ultra_conv.hip"]
+SOURCES = ["quant_kernels.hip", "gemm_w4a8.hip", "gemm_ws.hip", "gemm_wonly.hip", "attention.hip",
+           "qkv_attention.hip", "ultra_conv.hip"]
 HEADERS = ["qvit_common.h", "attn_common.h", "attn32.h", "ln_common.h", "diag_stamps.h"]
 
 HIPCC_FLAGS = [

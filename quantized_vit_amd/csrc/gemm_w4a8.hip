@@ -278,42 +278,65 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   const int nk = K / BK;  // even, >= 2
   // a tile's sources are uniform (m0, weight-tile base); the per-lane parts are tile-invariant
   // byte offsets from the A / Wp kernel arguments fit 32 bits (checked by the launcher)
-  struct Src {
-    int m0;
-    uint32_t w;  // the weight tile's byte offset in Wp
+  // LEAN (the fp32 / int32 epilogues): the per-lane parts of a tile's DMA sources (activation rows, clamped at
+  // the tail; the weight pieces' lane offset) and of its fragment reads are computed once per tile at its head,
+  // from an opaque lane id so that none of them stays live across the epilogue; a stage only moves the uniform
+  // SGPR bases (round 5: fc2 -2 %, measured). The int8-code epilogues need every register of the budget (their
+  // table lookups), so there the offsets are recomputed from the lane id at each use, as before (the lean form
+  // spilled).
+  constexpr bool LEAN = !I8OUT;
+  // per tile: the weight tile's byte offset in Wp (uniform) and the per-lane byte offsets from A of the tile's
+  // stage-0 activation pieces
+  uint32_t wlane = 0;
+  auto tile_w = [&](int tt) -> uint32_t {
+    return __builtin_amdgcn_readfirstlane((uint32_t)(tt % nb_n) * (uint32_t)(nk * G::WBYTES));
   };
-  auto tile_src = [&](int tt, Src& sr) {
-    sr.m0 = (tt / nb_n) * BM;
-    sr.w = (uint32_t)(tt % nb_n) * (uint32_t)(nk * G::WBYTES);
-  };
-  const uint32_t lds0 = lds_addr(smem);
-  auto issue = [&](const Src& sr, int kt, int rslot) {
-    const uint32_t sx = lds0 + (uint32_t)(rslot * G::STAGE);
-    const uint32_t sw = sx + XBYTES;
-    const uint32_t kx = (uint32_t)kt * BK;
-    const int lane_now = lane_opaque();
+  auto tile_a = [&](int tt, uint32_t (&a)[G::XPIECES], int ln) __attribute__((always_inline)) {
+    const int m0 = (tt / nb_n) * BM;
 #pragma unroll
     for (int j = 0; j < G::XPIECES; ++j) {
-      const int row = 32 * wave + 16 * j + (lane_now >> 2);
-      int gm = sr.m0 + row;
+      const int row = 32 * wave + 16 * j + (ln >> 2);
+      int gm = m0 + row;
       gm = gm < M ? gm : M - 1;  // clamp the tail: staged, never stored
-      const uint32_t lg = (uint32_t)(((lane_now & 3) ^ (((row >> 2) & 1) << 1)) * 16);
-      dma16s(A, (uint32_t)gm * (uint32_t)lda + lg + kx, __builtin_amdgcn_readfirstlane(sx + (32 * wave + 16 * j) * BK));
+      a[j] = (uint32_t)gm * (uint32_t)lda + (uint32_t)(((ln & 3) ^ (((row >> 2) & 1) << 1)) * 16);
     }
-    const uint32_t wt = sr.w + (uint32_t)kt * G::WBYTES + (uint32_t)(wave * (G::WPIECES * 1024) + lane_now * 16);
+  };
+  const uint32_t lds0 = lds_addr(smem);
+  auto issue = [&](int tt, uint32_t wt, const uint32_t (&a_in)[G::XPIECES], int kt, int rslot) __attribute__((always_inline)) {
+    const uint32_t sx = lds0 + (uint32_t)(rslot * G::STAGE);
+    const uint32_t sw = sx + XBYTES;
+    const int8_t* abase = A + kt * BK;
+    uint32_t a[G::XPIECES];
+    uint32_t wl = wlane;
+    if constexpr (LEAN) {
+#pragma unroll
+      for (int j = 0; j < G::XPIECES; ++j) a[j] = a_in[j];
+    } else {
+      const int ln = lane_opaque();
+      tile_a(tt, a, ln);
+      wl = (uint32_t)ln * 16u;
+    }
+#pragma unroll
+    for (int j = 0; j < G::XPIECES; ++j)
+      dma16s(abase, a[j], __builtin_amdgcn_readfirstlane(sx + (32 * wave + 16 * j) * BK));
+    const int8_t* wbase = Wp + wt + (uint32_t)kt * G::WBYTES + (uint32_t)(wave * (G::WPIECES * 1024));
+    // (piece j's 1-KiB step rides in the SGPR base: an instruction offset would move the LDS address too)
 #pragma unroll
     for (int j = 0; j < G::WPIECES; ++j)
-      dma16s(Wp, wt + j * 1024, __builtin_amdgcn_readfirstlane(sw + (WROWS_PER_WAVE * wave + WROWS_PER_PIECE * j) * G::WROW));
+      dma16s(wbase + j * 1024, wl, __builtin_amdgcn_readfirstlane(sw + (WROWS_PER_WAVE * wave + WROWS_PER_PIECE * j) * G::WROW));
   };
 
-  // per-lane fragment offsets inside a stage, recomputed from the lane id at each read (a few VALU per
-  // k-step) rather than held in registers across the register-bound main loop
-  auto read_frags = [&](int rslot, Frags<WFMT>& f) {
-    const int ln = lane_opaque();
+  // per-lane fragment offsets inside a stage (set at each tile head; one add per stage moves them to the slot)
+  int xoff = 0, woff = 0;
+  auto lane_offsets = [&](int ln) __attribute__((always_inline)) {
     const int lfr = ln & 15, lfq = ln >> 4;
-    const int xoff = (128 * wm + lfr) * BK + ((lfq ^ (((lfr >> 2) & 1) << 1)) << 4);
-    const int woff = (WFMT == QVIT_W4) ? (64 * wn + lfr) * G::WROW + ((lfq ^ (((lfr >> 3) & 1) << 1)) << 3)
-                                       : (64 * wn + lfr) * G::WROW + ((lfq ^ (((lfr >> 2) & 1) << 1)) << 4);
+    xoff = (128 * wm + lfr) * BK + ((lfq ^ (((lfr >> 2) & 1) << 1)) << 4);
+    woff = (WFMT == QVIT_W4) ? (64 * wn + lfr) * G::WROW + ((lfq ^ (((lfr >> 3) & 1) << 1)) << 3)
+                             : (64 * wn + lfr) * G::WROW + ((lfq ^ (((lfr >> 2) & 1) << 1)) << 4);
+    wlane = (uint32_t)ln * 16u;
+  };
+  auto read_frags = [&](int rslot, Frags<WFMT>& f) {
+    if constexpr (!LEAN) lane_offsets(lane_opaque());
     const int8_t* sx = smem + rslot * G::STAGE;
     const int8_t* sw = sx + XBYTES;
 #pragma unroll
@@ -328,7 +351,9 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   };
 
   v4i acc[4][8];
-  auto mfma_stage = [&](const Frags<WFMT>& f) {
+  // ZERO: the tile's first stage accumulates onto 0 (no register clearing per tile)
+  auto mfma_stage = [&](const Frags<WFMT>& f, auto zeroc) __attribute__((always_inline)) {
+    constexpr bool ZERO = decltype(zeroc)::value;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       v4i wf;
@@ -339,7 +364,8 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
         wf = f.w8[r];
       }
 #pragma unroll
-      for (int s = 0; s < 8; ++s) acc[r][s] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wf, f.x[s], acc[r][s], 0, 0, 0);
+      for (int s = 0; s < 8; ++s)
+        acc[r][s] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wf, f.x[s], ZERO ? v4i{0, 0, 0, 0} : acc[r][s], 0, 0, 0);
     }
   };
 
@@ -347,10 +373,11 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   // The phases are fenced (sched_barrier) and the LDS drain at the top is compiler-visible, so the
   // fragment reads of stage kt+1 overlap the MFMAs of stage kt with no wait between them.
   constexpr int D = G::DMA_PER_STAGE;
-  auto step_core = [&](Frags<WFMT>& cur, Frags<WFMT>& nxt, int next_slot, bool read) __attribute__((always_inline)) {
+  auto step_core = [&](Frags<WFMT>& cur, Frags<WFMT>& nxt, int next_slot, bool read,
+                       auto zeroc) __attribute__((always_inline)) {
     if (read) read_frags(next_slot, nxt);
     __builtin_amdgcn_sched_barrier(0);
-    mfma_stage(cur);
+    mfma_stage(cur, zeroc);
     __builtin_amdgcn_sched_barrier(0);
   };
 
@@ -459,23 +486,30 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     else job(std::integral_constant<int, 4>{}, std::integral_constant<int, 1>{});
   };
 
-  Src cs, ns;
-  tile_src(t, cs);
-  // prologue: the first tile's stages 0 and 1
+  // prologue: the first tile's stages 0 and 1 (the Src values are scoped to one tile: nothing of them is
+  // carried across a loop iteration)
   int g = 0;  // global stage counter of this block (ring slot = g % RING)
-  issue(cs, 0, 0);
-  issue(cs, 1, 1);
+  {
+    uint32_t a0[G::XPIECES];
+    lane_offsets(lane_opaque());
+    tile_a(t, a0, lane_opaque());
+    const uint32_t w0 = tile_w(t);
+    issue(t, w0, a0, 0, 0);
+    issue(t, w0, a0, 1, 1);
+  }
   Frags<WFMT> fa, fb;
   QVIT_STAMP_DECL
+  QVIT_LSTAMP_DECL
   for (;;) {
     const int tnext = t + team;
     const bool has_next = tnext < hi;
-    if (has_next) tile_src(tnext, ns);
     const int m0 = (t / nb_n) * BM, n0 = (t % nb_n) * BN;
+    if (nk == 2 || !LEAN) {  // (K = 128: no steady step, the tail's first stage is the tile's first)
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+      for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int s = 0; s < 8; ++s) acc[r][s] = v4i{0, 0, 0, 0};
+        for (int s = 0; s < 8; ++s) acc[r][s] = v4i{0, 0, 0, 0};
+    }
 
     // head: stage 0 of this tile landed (stage 1 may still be in flight); every wave is past the
     // previous tile's epilogue, so the tile's bias can be DMA'd into its LDS slot (1 KiB, wave 0;
@@ -484,44 +518,75 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     __builtin_amdgcn_s_waitcnt(0xC07F);
     stage_sync<D>();
     QVIT_STAMP(0);
-    if (has_bias && wave == 0)
-      dma16(ep.bias + n0 + lane_opaque() * 4, __builtin_amdgcn_readfirstlane(lds0 + G::RING_BYTES + G::EPI_BYTES));
+    QVIT_LSTAMP(0);
+    uint32_t ca[G::XPIECES];
+    const uint32_t cw = tile_w(t);
+    {
+      const int ln = lane_opaque();
+      lane_offsets(ln);
+      tile_a(t, ca, ln);
+      if (has_bias && wave == 0)
+        dma16(ep.bias + n0 + ln * 4, __builtin_amdgcn_readfirstlane(lds0 + G::RING_BYTES + G::EPI_BYTES));
+    }
     read_frags(g % RING, fa);
-    // steady steps kt = 0 .. nk-3: issue this tile's stage kt+2
+    // steady steps kt = 0 .. nk-3: issue this tile's stage kt+2 (the first one peeled: zero accumulators)
     int kt = 0;
-    for (; kt < nk - 2; kt += 2) {
+    if (LEAN && nk > 2) {
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_sched_barrier(0);
-      issue(cs, kt + 2, (g + kt + 2) % RING);
+      issue(t, cw, ca, 2, (g + 2) % RING);
       QVIT_STAMP(1);
       stage_sync<D>();
       QVIT_STAMP(2);
-      step_core(fa, fb, (g + kt + 1) % RING, true);
+      step_core(fa, fb, (g + 1) % RING, true, std::true_type{});
       QVIT_STAMP(3);
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_sched_barrier(0);
-      issue(cs, kt + 3, (g + kt + 3) % RING);
+      issue(t, cw, ca, 3, (g + 3) % RING);
       QVIT_STAMP(1);
       stage_sync<D>();
       QVIT_STAMP(2);
-      step_core(fb, fa, (g + kt + 2) % RING, true);
+      step_core(fb, fa, (g + 2) % RING, true, std::false_type{});
+      QVIT_STAMP(3);
+      kt = 2;
+    }
+    for (; kt < nk - 2; kt += 2) {
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_sched_barrier(0);
+      issue(t, cw, ca, kt + 2, (g + kt + 2) % RING);
+      QVIT_STAMP(1);
+      stage_sync<D>();
+      QVIT_STAMP(2);
+      step_core(fa, fb, (g + kt + 1) % RING, true, std::false_type{});
+      QVIT_STAMP(3);
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_sched_barrier(0);
+      issue(t, cw, ca, kt + 3, (g + kt + 3) % RING);
+      QVIT_STAMP(1);
+      stage_sync<D>();
+      QVIT_STAMP(2);
+      step_core(fb, fa, (g + kt + 2) % RING, true, std::false_type{});
       QVIT_STAMP(3);
     }
     // tail kt = nk-2, nk-1: issue the next tile's stages 0, 1
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_sched_barrier(0);
+    uint32_t na[G::XPIECES];
+    const uint32_t nw = has_next ? tile_w(tnext) : 0u;
     if (has_next) {
-      issue(ns, 0, (g + nk) % RING);
+      tile_a(tnext, na, lane_opaque());  // (here, not at the tile head: this tile's offsets are dead by now)
+      issue(tnext, nw, na, 0, (g + nk) % RING);
       stage_sync<D>();
     } else {
       stage_sync<0>();
     }
-    step_core(fa, fb, (g + nk - 1) % RING, true);
+    step_core(fa, fb, (g + nk - 1) % RING, true, std::false_type{});
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_sched_barrier(0);
-    if (has_next) issue(ns, 1, (g + nk + 1) % RING);
-    step_core(fb, fa, 0, false);
+    if (has_next) issue(tnext, nw, na, 1, (g + nk + 1) % RING);
+    step_core(fb, fa, 0, false, std::false_type{});
     QVIT_STAMP(3);
+    QVIT_LSTAMP(1);
 
     if (WFMT == QVIT_W4 && EPI == QVIT_EPI_I32) {  // 16 acc -> acc (exact arithmetic shift)
 #pragma unroll
@@ -554,27 +619,34 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
       }
       // 16-B row stores when every row segment is whole and aligned (kernel-uniform); else byte stores
       const bool fast16 = ((ldc & 15) == 0) && ((((uintptr_t)C) & 15) == 0) && ((N & 15) == 0);
-#pragma unroll
-      for (int sr = 0; sr < 8; ++sr) {
-        const int m = m0 + 128 * wm + 16 * sr + efr;
-        uint32_t wd[4];
-        // the row's 16 lookups are issued together, then resolved (one LDS latency per row)
-        float v[4][4];
-        uint2 e[4][4];
+      // software-pipelined over the 8 rows: row sr + 1's 16 lookups are issued before row sr's are resolved, so
+      // each row's LDS latency runs under the previous row's selects and store (the fragment registers of the
+      // main loop are free here: two rows of values and entries fit beside the accumulators)
+      float v[2][4][4];
+      uint2 e[2][4][4];
+      auto look = [&](int sr, int b) __attribute__((always_inline)) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            v[r][j] = fmaf(alpha, (float)acc[r][sr][j], bcol[4 * r + j]);
-            e[r][j] = *epi_entry(tlb, v[r][j], t_c0, t_invw, t_top);
+            v[b][r][j] = fmaf(alpha, (float)acc[r][sr][j], bcol[4 * r + j]);
+            e[b][r][j] = *epi_entry(tlb, v[b][r][j], t_c0, t_invw, t_top);
           }
+      };
+      look(0, 0);
+#pragma unroll
+      for (int sr = 0; sr < 8; ++sr) {
+        const int cb = sr & 1;
+        if (sr + 1 < 8) look(sr + 1, cb ^ 1);
         __builtin_amdgcn_sched_barrier(0);
+        const int m = m0 + 128 * wm + 16 * sr + efr;
+        uint32_t wd[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          epi_select_byte<0>(wd[r], v[r][0], __uint_as_float(e[r][0].x), e[r][0].y);
-          epi_select_byte<1>(wd[r], v[r][1], __uint_as_float(e[r][1].x), e[r][1].y);
-          epi_select_byte<2>(wd[r], v[r][2], __uint_as_float(e[r][2].x), e[r][2].y);
-          epi_select_byte<3>(wd[r], v[r][3], __uint_as_float(e[r][3].x), e[r][3].y);
+          epi_select_byte<0>(wd[r], v[cb][r][0], __uint_as_float(e[cb][r][0].x), e[cb][r][0].y);
+          epi_select_byte<1>(wd[r], v[cb][r][1], __uint_as_float(e[cb][r][1].x), e[cb][r][1].y);
+          epi_select_byte<2>(wd[r], v[cb][r][2], __uint_as_float(e[cb][r][2].x), e[cb][r][2].y);
+          epi_select_byte<3>(wd[r], v[cb][r][3], __uint_as_float(e[cb][r][3].x), e[cb][r][3].y);
         }
         int8_t* dst = reinterpret_cast<int8_t*>(C) + (int64_t)m * ldc + nbase;
         if (fast16) {
@@ -584,6 +656,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
           for (int q = 0; q < 16; ++q)
             if (nbase + q < N) dst[q] = (int8_t)((wd[q >> 2] >> (8 * (q & 3))) & 0xff);
         }
+        __builtin_amdgcn_sched_barrier(0);
       }
     } else if (EPI == QVIT_EPI_F32_RESID || EPI == EPI_RESID_LN) {
       // C += alpha acc + bias: 16 rows per pass through the wave's staging area, 16 lanes per 64-column
@@ -810,16 +883,17 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     }
     if (I8OUT) __builtin_amdgcn_s_setprio(0);
     QVIT_STAMP(4);
+    QVIT_LSTAMP(2);
     if constexpr (EPI == EPI_RESID_LN) {
       ln_after_tile(m0);
       QVIT_STAMP(6);
     }
     if (!has_next) break;
     t = tnext;
-    cs = ns;
     g += nk;
   }
   QVIT_STAMP_FLUSH;
+  QVIT_LSTAMP_FLUSH;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -885,6 +959,12 @@ int dispatch_epi(int epilogue, const int8_t* A, int64_t M, int64_t K, int64_t ld
 
 }  // namespace
 
+// gemm_ws.hip: the weight-stationary schedule of the int8-code epilogues for the shapes it fits (1: launched)
+int qvit_gemm_ws_try(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int64_t N, int64_t npad,
+                     const float* d_act, const float* d_wt, const float* bias, int epilogue, void* C, int64_t ldc,
+                     int out_qtype, const float* out_d, const float* out_qm, const float* out_t, int out_levels,
+                     const void* epi_table, hipStream_t stream);
+
 extern "C" int qvit_epi_table_build(int epilogue, int out_qtype, const float* out_d, const float* out_qm,
                                     const float* out_t, int out_levels, float v_lo, float w, int64_t nb, void* table,
                                     hipStream_t stream) {
@@ -933,7 +1013,14 @@ extern "C" int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda, con
   if (epi_table && (((uintptr_t)epi_table) & 15)) return QVIT_EALIGN;
   EpiArgs ep{d_act, d_wt, bias, out_qtype, out_d, out_qm, out_t, out_levels,
              (i8out ? reinterpret_cast<const int8_t*>(epi_table) : nullptr), 1, 1.f, 1.f, nullptr};
-  if (wfmt == QVIT_W4) return dispatch_epi<QVIT_W4>(epilogue, A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
+  if (wfmt == QVIT_W4) {
+#ifdef QVIT_GEMM_WS  // (weight-stationary schedule: under evaluation, off in the product build)
+    const int ws = qvit_gemm_ws_try(A, M, K, lda, Wp, N, npad, d_act, d_wt, bias, epilogue, C, ldc, out_qtype, out_d,
+                                    out_qm, out_t, out_levels, epi_table, stream);
+    if (ws != 0) return ws == 1 ? QVIT_OK : ws;
+#endif
+    return dispatch_epi<QVIT_W4>(epilogue, A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
+  }
   return dispatch_epi<QVIT_W8>(epilogue, A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
 }
 

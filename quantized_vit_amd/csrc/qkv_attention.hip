@@ -333,7 +333,7 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
     // unit's DMA pieces and activation loads stay in flight under the attention)
     __builtin_amdgcn_s_waitcnt(0xC07F);
     asm volatile("s_barrier" ::: "memory");
-    sp.mark(9);
+    sp.mark(6);
 
     // ---- 3. attention over the resident K / V ------------------------------------------------------
     // q as the 32-query tile's B operands: lane group G (tile G & 1, dims 32 (G >> 1) .. + 31) takes the

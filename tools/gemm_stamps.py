@@ -30,7 +30,17 @@ def main():
     ap.add_argument("--build-var", nargs="*", default=[],
                     help="NAME=DEF1,DEF2 ...: build tools/_diag/libqvit_hip_NAME.so with those defines")
     ap.add_argument("--bench-var", default="", help="time variant library NAME (see --build-var)")
+    ap.add_argument("--ws", default="", help="a -DQVIT_GEMM_WS_STAMPS build (path): the weight-stationary kernel's "
+                    "per-tile k-loop / epilogue cycles, weight fill and clock")
+    ap.add_argument("--light", default="", help="a -DQVIT_GEMM_LSTAMPS build (path): per-tile head / main loop / "
+                    "epilogue cycles and the in-kernel clock")
     a = ap.parse_args()
+    if a.light:
+        light(a)
+        return
+    if a.ws:
+        ws(a)
+        return
     from quantized_vit_amd import build
     if a.build_var:
         for spec in a.build_var:
@@ -79,6 +89,61 @@ def main():
         mfma_cyc = int(32 * nk * 16 * tiles / blocks)  # 32 MFMAs of 16 cycles per stage, per wave
         print(f"{name:8s} {r['ms']*1e3:7.1f} us  cycles/wave {tot:9.0f}  (MFMA floor {mfma_cyc})  " +
               "  ".join(f"{p} {v:7.0f} ({100*v/tot:4.1f}%)" for p, v in zip(PHASES, per)), flush=True)
+
+
+def light(a):
+    """Per-tile phase cycles from a light-stamp build: three s_memtime stamps per tile (no per-stage stamp, so the
+    main loop runs as in the product), and the in-kernel clock from s_memtime / s_memrealtime (100 MHz)."""
+    import torch
+    from quantized_vit_amd import _lib
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import gemm_bench
+    lib = _lib.load(a.light)
+    lib.qvit_gemm_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.qvit_gemm_stamps.restype = ctypes.c_int
+    dev = torch.device("cuda:0")
+    buf = (ctypes.c_ulonglong * 8)()
+    for name in a.shapes.split(","):
+        M, N, K, epi = gemm_bench.SHAPES[name]
+        gemm_bench.run(name, M, N, K, epi, 3, dev)  # warm
+        torch.cuda.synchronize()
+        assert lib.qvit_gemm_stamps(buf, 1) == 0
+        r = gemm_bench.run(name, M, N, K, epi, a.iters, dev)
+        torch.cuda.synchronize()
+        assert lib.qvit_gemm_stamps(buf, 0) == 0
+        tiles = max(buf[5], 1)
+        nk = K // 64
+        floor = 32 * nk * 16  # one wave's MFMA cycles per tile (16 per 16x16x64 MFMA, 32 per stage)
+        clk = buf[3] / max(buf[4], 1) * 0.1
+        print(f"{name:8s} {r['ms']*1e3:7.1f} us  clock {clk:5.2f} GHz  per tile and wave: head {buf[0]/tiles:7.0f}  "
+              f"main loop {buf[1]/tiles:7.0f} (MFMA alone {floor})  epilogue {buf[2]/tiles:7.0f}  "
+              f"tiles/wave {tiles/max(buf[7],1):5.2f}  wave life {buf[3]/max(buf[7],1):9.0f} cyc", flush=True)
+
+
+def ws(a):
+    import torch
+    from quantized_vit_amd import _lib
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import gemm_bench
+    lib = _lib.load(a.ws)
+    lib.qvit_gemm_ws_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.qvit_gemm_ws_stamps.restype = ctypes.c_int
+    dev = torch.device("cuda:0")
+    buf = (ctypes.c_ulonglong * 8)()
+    for name in a.shapes.split(","):
+        M, N, K, epi = gemm_bench.SHAPES[name]
+        gemm_bench.run(name, M, N, K, epi, 3, dev)
+        torch.cuda.synchronize()
+        assert lib.qvit_gemm_ws_stamps(buf, 1) == 0
+        r = gemm_bench.run(name, M, N, K, epi, a.iters, dev)
+        torch.cuda.synchronize()
+        assert lib.qvit_gemm_ws_stamps(buf, 0) == 0
+        tiles, waves = max(buf[5], 1), max(buf[7], 1)
+        floor = (K // 32) * 6 * 32  # one wave's 32x32x32 MFMA cycles per 64 x 96 tile
+        clk = buf[3] / max(buf[4], 1) * 0.1
+        print(f"{name:8s} {r['ms']*1e3:7.1f} us  clock {clk:5.2f} GHz  per tile and wave: k-loop {buf[0]/tiles:7.0f} "
+              f"(MFMA alone {floor})  epilogue {buf[1]/tiles:7.0f}  fill {buf[2]/waves:7.0f}  tiles/wave "
+              f"{tiles/waves:5.2f}  wave life {buf[3]/waves:9.0f} cyc", flush=True)
 
 
 if __name__ == "__main__":
