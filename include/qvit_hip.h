@@ -198,6 +198,33 @@ int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda,
               int out_levels, const void* epi_table, hipStream_t stream);
 
 /*
+ * QVIT_ACT_T32: activation codes in the operand order of the int8 32x32x32 matrix instruction, the input of
+ * qvit_gemm_a32. An [M][kpad] code matrix (kpad % 64 == 0) is stored as 1-KiB blocks of 32 rows x 32 columns,
+ * block (r / 32, c / 32) at byte (r / 32 * kpad / 32 + c / 32) * 1024; inside it, 16-byte group
+ * (r % 32) + 32 * ((c / 16) % 2) holds columns c - c % 16 .. + 15 of row r. Buffers hold ceil(M / 64) * 64 rows
+ * (rows past M are never stored).
+ *
+ * qvit_layernorm_quant_i8_t32: qvit_layernorm_quant_i8 (vit_model.py:206-207 norm2 + the fc1 layer's quantize_act,
+ *   quant_layers.py:356-381) with the codes written in QVIT_ACT_T32 order: cols % 4 == 0, cols <= 1024,
+ *   kpad % 64 == 0, x / gamma / beta / codes 16-byte aligned. Same codes as qvit_layernorm_quant_i8, byte for byte.
+ * qvit_gemm_a32: qvit_gemm with the activations in QVIT_ACT_T32 order, for the int8-code epilogues of Mlp.fc1
+ *   (quant_layers.py:495-499 under vit_model.py:172: GELU + fc2's quantizer): a weight-stationary schedule (each
+ *   CU holds one 96-row panel of the int4 weights in LDS for the whole launch) on int8 32x32x32 MFMA. Same codes
+ *   as qvit_gemm on the row-major codes, byte for byte. Shapes: qvit_gemm_a32_fits (wfmt QVIT_W4, epilogue
+ *   QVIT_EPI_I8 / QVIT_EPI_I8_GELU, N == npad == 3072, K == 768 or 1024) returns 1, else the call is QVIT_EINVAL.
+ *   C: int8 [M][ldc], ldc % 16 == 0, 16-byte aligned.
+ */
+int qvit_layernorm_quant_i8_t32(const float* x, int64_t rows, int64_t cols, int64_t ldx, const float* gamma,
+                                const float* beta, float eps, int qtype, const float* d_quant, const float* q_m,
+                                const float* t_quant, int levels, int8_t* codes, int64_t kpad,
+                                const void* code_table, hipStream_t stream);
+int qvit_gemm_a32_fits(int64_t K, int wfmt, int64_t N, int64_t npad, int epilogue);
+int qvit_gemm_a32(const int8_t* A, int64_t M, int64_t K, const void* Wp, int wfmt, int64_t N, int64_t npad,
+                  const float* d_act, const float* d_wt, const float* bias, int epilogue, void* C, int64_t ldc,
+                  int out_qtype, const float* out_d, const float* out_qm, const float* out_t, int out_levels,
+                  const void* epi_table, hipStream_t stream);
+
+/*
  * Weight-only QuantizeLinear.forward (quant_layers.py:495-499, quant_mode WEIGHT_ONLY: quantize_act is the
  * identity, :356-358): Y[m, n] = d_wt * sum_k X[m, k] k_w[n, k] + bias[n] with fp32 X.
  *   X      : fp32 [M][ldx], K valid columns; K % QVIT_TILE_K == 0 (pad X with zero columns to the packed

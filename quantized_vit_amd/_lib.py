@@ -65,6 +65,11 @@ _SIGNATURES = {
                                 _c_p, _i64, _i64, _c_p, _c_p],
     "qvit_gemm": [_c_p, _i64, _i64, _i64, _c_p, _i32, _i64, _i64, _c_p, _c_p, _c_p, _i32, _c_p, _i64,
                   _i32, _c_p, _c_p, _c_p, _i32, _c_p, _c_p],
+    "qvit_layernorm_quant_i8_t32": [_c_p, _i64, _i64, _i64, _c_p, _c_p, _f32, _i32, _c_p, _c_p, _c_p, _i32, _c_p,
+                                    _i64, _c_p, _c_p],
+    "qvit_gemm_a32_fits": [_i64, _i32, _i64, _i64, _i32],
+    "qvit_gemm_a32": [_c_p, _i64, _i64, _c_p, _i32, _i64, _i64, _c_p, _c_p, _c_p, _i32, _c_p, _i64, _i32, _c_p, _c_p,
+                      _c_p, _i32, _c_p, _c_p],
     "qvit_gemm_wonly": [_c_p, _i64, _i64, _i64, _c_p, _i32, _i64, _i64, _c_p, _c_p, _c_p, _i64, _c_p, _i64, _c_p],
     "qvit_conv_wonly": [_c_p, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _c_p, _i32,
                         _i64, _i64, _i64, _c_p, _c_p, _c_p, _c_p, _i64, _c_p],
@@ -114,6 +119,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
                 "(the HIP extension is required; there is no CPU fallback)")
         lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
         for name, args in _SIGNATURES.items():
+            if path != LIB_PATH and not hasattr(lib, name):
+                continue  # an older build loaded for a same-box A/B (tools/lib_ab.sh): its entry points only
             fn = getattr(lib, name)
             fn.argtypes = args
             fn.restype = ctypes.c_int
@@ -279,6 +286,60 @@ def gemm(A: torch.Tensor, M: int, K: int, packed: torch.Tensor, wfmt: int, N: in
     _check(load().qvit_gemm(_ptr(A), M, K, A.stride(0), _ptr(packed), wfmt, N, npad, _ptr(d_act), _ptr(d_wt),
                             _ptr(bias_pad), epilogue, _ptr(C), C.stride(0), out_qtype, _ptr(out_d), _ptr(out_qm),
                             _ptr(out_t), out_levels, _ptr(epi_table), _stream(A.device)), "qvit_gemm")
+    return C
+
+
+def t32_rows(M: int) -> int:
+    """Rows a QVIT_ACT_T32 code buffer holds for M rows (whole 64-row wave tiles of qvit_gemm_a32)."""
+    return (M + 63) // 64 * 64
+
+
+def t32_to_rows(codes_t32: torch.Tensor, M: int, kpad: int) -> torch.Tensor:
+    """QVIT_ACT_T32 codes -> row-major [M, kpad] (a view permutation; tests and code tracing only)."""
+    R = t32_rows(M)
+    t = codes_t32.view(-1)[:R * kpad].view(R // 32, kpad // 32, 2, 32, 16)   # [rb][kb][half][row][16]
+    return t.permute(0, 3, 1, 2, 4).reshape(R, kpad)[:M]
+
+
+def rows_to_t32(codes: torch.Tensor, kpad: int) -> torch.Tensor:
+    """Row-major [M, >= kpad] codes -> a QVIT_ACT_T32 buffer (rows padded with zeros; tests only)."""
+    M = codes.shape[0]
+    R = t32_rows(M)
+    full = torch.zeros((R, kpad), dtype=torch.int8, device=codes.device)
+    full[:M] = codes[:, :kpad]
+    return full.view(R // 32, 32, kpad // 32, 2, 16).permute(0, 2, 3, 1, 4).contiguous().view(-1)
+
+
+def layernorm_quant_i8_t32(x2d: torch.Tensor, gamma: Optional[torch.Tensor], beta: Optional[torch.Tensor], eps: float,
+                           qtype: int, d, qm, t, levels: int, out: torch.Tensor, kpad: int,
+                           code_table: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """layernorm_quant_i8 with the codes in QVIT_ACT_T32 order (out: int8, >= t32_rows(M) * kpad bytes)."""
+    _require_gpu(x2d, "input")
+    assert x2d.dtype == torch.float32 and x2d.stride(1) == 1
+    rows, cols = x2d.shape
+    assert out.numel() >= t32_rows(rows) * kpad
+    _check(load().qvit_layernorm_quant_i8_t32(_ptr(x2d), rows, cols, x2d.stride(0), _ptr(gamma), _ptr(beta), eps,
+                                              qtype, _ptr(d), _ptr(qm), _ptr(t), levels, _ptr(out), kpad,
+                                              _ptr(code_table), _stream(x2d.device)), "qvit_layernorm_quant_i8_t32")
+    return out
+
+
+def gemm_a32_fits(K: int, wfmt: int, N: int, npad: int, epilogue: int) -> bool:
+    lib = load()
+    if not hasattr(lib, "qvit_gemm_a32_fits"):  # (an older build in a same-box A/B)
+        return False
+    return bool(lib.qvit_gemm_a32_fits(K, wfmt, N, npad, epilogue))
+
+
+def gemm_a32(A: torch.Tensor, M: int, K: int, packed: torch.Tensor, wfmt: int, N: int, npad: int, d_act, d_wt,
+             bias_pad: Optional[torch.Tensor], epilogue: int, C: torch.Tensor, out_qtype: int = 0, out_d=None,
+             out_qm=None, out_t=None, out_levels: int = 0, epi_table: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """qvit_gemm_a32: the int8-code GEMM on QVIT_ACT_T32 activations (weight-stationary fc1 schedule)."""
+    _require_gpu(A, "codes")
+    assert A.numel() >= t32_rows(M) * K
+    _check(load().qvit_gemm_a32(_ptr(A), M, K, _ptr(packed), wfmt, N, npad, _ptr(d_act), _ptr(d_wt), _ptr(bias_pad),
+                                epilogue, _ptr(C), C.stride(0), out_qtype, _ptr(out_d), _ptr(out_qm), _ptr(out_t),
+                                out_levels, _ptr(epi_table), _stream(A.device)), "qvit_gemm_a32")
     return C
 
 

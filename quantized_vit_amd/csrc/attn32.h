@@ -32,32 +32,6 @@ QVIT_DEV f16x mfma3w(h8 ah, h8 al, h8 bh, h8 bl, f16x c) {
 // keeps the same swizzle (an immediate offset); the epilogue's 16-B writes are 2-way
 QVIT_DEV int v32off(int r, int byte) { return r * 128 + (byte ^ (((((r >> 1) & 1) << 2) | ((r >> 2) & 1)) << 4)); }
 
-// P's fp16 hi/lo split with the same values as attn_common.h split8 (hi = RNE f16 of x; lo = RNE f16 of the
-// exact f32 x - hi) in fewer VALU: lo comes from v_fma_mix{lo,hi}_f16 (-hi as an f16 source, x as f32, one
-// rounding of the exact difference) instead of cvt f16 -> f32, subtract and cvt back. The asm carries its own
-// wait states: s_nop 0 first (x is fresh from v_exp: transcendental -> VALU use), s_nop 1 last (its results
-// are MFMA operands: VALU write -> MFMA read).
-QVIT_DEV void split8_mix(const float (&x)[8], h8& hi, h8& lo) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) hi[i] = (_Float16)x[i];
-  const u4 hw = __builtin_bit_cast(u4, hi);
-  u4 lw;
-  asm("s_nop 0\n\t"
-      "v_fma_mixlo_f16 %0, -%4, 1.0, %8 op_sel_hi:[1,0,0]\n\t"
-      "v_fma_mixhi_f16 %0, -%4, 1.0, %9 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
-      "v_fma_mixlo_f16 %1, -%5, 1.0, %10 op_sel_hi:[1,0,0]\n\t"
-      "v_fma_mixhi_f16 %1, -%5, 1.0, %11 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
-      "v_fma_mixlo_f16 %2, -%6, 1.0, %12 op_sel_hi:[1,0,0]\n\t"
-      "v_fma_mixhi_f16 %2, -%6, 1.0, %13 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
-      "v_fma_mixlo_f16 %3, -%7, 1.0, %14 op_sel_hi:[1,0,0]\n\t"
-      "v_fma_mixhi_f16 %3, -%7, 1.0, %15 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
-      "s_nop 1"
-      : "=&v"(lw[0]), "=&v"(lw[1]), "=&v"(lw[2]), "=&v"(lw[3])
-      : "v"(hw[0]), "v"(hw[1]), "v"(hw[2]), "v"(hw[3]), "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]),
-        "v"(x[5]), "v"(x[6]), "v"(x[7]));
-  lo = __builtin_bit_cast(h8, lw);
-}
-
 QVIT_DEV float bits_f(uint32_t u) { return __uint_as_float(u); }
 QVIT_DEV float pair_max(float v) {
   const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);

@@ -959,12 +959,6 @@ int dispatch_epi(int epilogue, const int8_t* A, int64_t M, int64_t K, int64_t ld
 
 }  // namespace
 
-// gemm_ws.hip: the weight-stationary schedule of the int8-code epilogues for the shapes it fits (1: launched)
-int qvit_gemm_ws_try(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int64_t N, int64_t npad,
-                     const float* d_act, const float* d_wt, const float* bias, int epilogue, void* C, int64_t ldc,
-                     int out_qtype, const float* out_d, const float* out_qm, const float* out_t, int out_levels,
-                     const void* epi_table, hipStream_t stream);
-
 extern "C" int qvit_epi_table_build(int epilogue, int out_qtype, const float* out_d, const float* out_qm,
                                     const float* out_t, int out_levels, float v_lo, float w, int64_t nb, void* table,
                                     hipStream_t stream) {
@@ -1013,14 +1007,7 @@ extern "C" int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda, con
   if (epi_table && (((uintptr_t)epi_table) & 15)) return QVIT_EALIGN;
   EpiArgs ep{d_act, d_wt, bias, out_qtype, out_d, out_qm, out_t, out_levels,
              (i8out ? reinterpret_cast<const int8_t*>(epi_table) : nullptr), 1, 1.f, 1.f, nullptr};
-  if (wfmt == QVIT_W4) {
-#ifdef QVIT_GEMM_WS  // (weight-stationary schedule: under evaluation, off in the product build)
-    const int ws = qvit_gemm_ws_try(A, M, K, lda, Wp, N, npad, d_act, d_wt, bias, epilogue, C, ldc, out_qtype, out_d,
-                                    out_qm, out_t, out_levels, epi_table, stream);
-    if (ws != 0) return ws == 1 ? QVIT_OK : ws;
-#endif
-    return dispatch_epi<QVIT_W4>(epilogue, A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
-  }
+  if (wfmt == QVIT_W4) return dispatch_epi<QVIT_W4>(epilogue, A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
   return dispatch_epi<QVIT_W8>(epilogue, A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
 }
 

@@ -13,7 +13,11 @@
 //     into the XCD's L2 once and read by all 32 CUs from there;
 //   * each wave owns 64-row tiles (rows 64 i .. + 63, i = its XCD range's wave-tiles w, w + 8, ...) and streams their
 //     activation fragments straight from global memory into registers, two 64-deep stages ahead (no LDS-DMA, no
-//     barrier: the waves of a CU never wait for each other after the weight fill);
+//     barrier: the waves of a CU never wait for each other after the weight fill). The activations come in the
+//     MFMA operand order (QVIT_ACT_T32, written by the producing LayerNorm, qvit_layernorm_quant_i8_t32): every
+//     fragment load is one contiguous KiB. (Loaded from row-major codes, each lane of a fragment load is its own
+//     row, 63 L1 accesses per instruction: the texture path was 78 % busy and the k-loop ran at 4.7x its MFMA
+//     time, round-5 PMC and stamps.)
 //   * v_mfma_i32_32x32x32_i8 (32 cycles, holds vector issue for 8): the SIMD partner's epilogue VALU gets three
 //     quarters of the issue slots instead of half.
 // Operand maps (tools/calib/mfma_i8_32x32_maps.hip, exact): lane l holds A[l & 31][16 (l >> 5) + j] and
@@ -47,6 +51,13 @@ constexpr int WS_WAVES = 8;
 #define QVIT_WS_PD 2
 #endif
 constexpr int PD = QVIT_WS_PD;  // 64-deep activation stages loaded ahead of the one computing
+// stages loaded as one group: the loads of a group touch each 128-B line of its rows back to back (pairs of 64-B
+// stage chunks), so the L1 serves all but the first of them; loaded one stage at a time a line's second half was
+// evicted before its turn (the k-loop ran at 4.7x its MFMA time, round-5 stamps)
+#ifndef QVIT_WS_GS
+#define QVIT_WS_GS 2
+#endif
+constexpr int GS = QVIT_WS_GS;
 constexpr int WS_NT = WS_WAVES * 64;
 constexpr int WS_TBL_BYTES = 17408;                       // code table region (<= 2174 buckets, as gemm_kernel)
 constexpr int WS_TABLE_MAX_NB = (WS_TBL_BYTES - 16) / 8;
@@ -84,7 +95,7 @@ QVIT_DEV uint32_t w4_image_offset(int n, int st, int c, int nk) {
 }
 
 template <int NTN, int NKC, int EPI>
-__global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(const int8_t* __restrict__ A, int M, int64_t lda,
+__global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(const int8_t* __restrict__ A, int M,
                                                            const int8_t* __restrict__ Wp, int8_t* __restrict__ C,
                                                            int64_t ldc, int panels, WsArgs ep) {
   using G = WsGeo<NTN, NKC>;
@@ -111,15 +122,22 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(const int8_t* __restr
   // quantizer's code table and scalars
   {
     constexpr int SLOTS = G::FRAGS * 64;  // 16-B fragment slots
-    for (int q = tid; q < SLOTS; q += WS_NT) {
+    constexpr int PER = SLOTS / WS_NT;
+    static_assert(SLOTS % WS_NT == 0, "fill slots per thread");
+    uint2 p[PER];  // all of a thread's loads in flight together
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int q = tid + j * WS_NT;
       const int f = q >> 6, l = q & 63;
       const int kh = f & 1, u = (f >> 1) % NTN, st = (f >> 1) / NTN;
       const int i = l & 31, h = l >> 5;
       const int n = n0 + 32 * u + 16 * ((i >> 2) & 1) + 4 * (i >> 3) + (i & 3);
-      const uint2 p = *reinterpret_cast<const uint2*>(Wp + w4_image_offset(n, st, 2 * kh + h, NKC));
-      *reinterpret_cast<v4i*>(wl + q * 16) =
-          v4i{(int)nib16_lo(p.x), (int)nib16_hi(p.x), (int)nib16_lo(p.y), (int)nib16_hi(p.y)};
+      p[j] = *reinterpret_cast<const uint2*>(Wp + w4_image_offset(n, st, 2 * kh + h, NKC));
     }
+#pragma unroll
+    for (int j = 0; j < PER; ++j)
+      *reinterpret_cast<v4i*>(wl + (tid + j * WS_NT) * 16) =
+          v4i{(int)nib16_lo(p[j].x), (int)nib16_hi(p[j].x), (int)nib16_lo(p[j].y), (int)nib16_hi(p[j].y)};
     for (int j = tid; j < PW; j += WS_NT) bias_l[j] = ep.bias ? ep.bias[n0 + j] : 0.f;
   }
   bool use_table = false;
@@ -152,21 +170,13 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(const int8_t* __restr
 
   const int lane = tid & 63;
   const int lr = lane & 31, lh = lane >> 5;
-  // per-lane activation offsets of a tile's two 32-row MFMA tiles (rows past M read row M - 1: loaded, never stored)
+  // T32 activations: the 1-KiB block of rows 32 mb .. + 31, k 32 kb .. + 31 at (mb KB32 + kb) KiB, lane l's 16 B at
+  // 16 l (rows past M exist in the padded buffer: loaded, never stored); per tile one uniform offset
+  const uint32_t kb32 = (uint32_t)(NKC * 2);
+  const uint32_t lane16 = (uint32_t)lane * 16u;
   auto aoffs = [&](int i, uint32_t (&o)[2]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      int m = 64 * i + 32 * t + lr;
-      m = m < M ? m : M - 1;
-      o[t] = (uint32_t)m * (uint32_t)lda + (uint32_t)(16 * lh);
-    }
-  };
-  // activation fragments of stage s: x[t][kh] = A[m_t][64 s + 32 kh + 16 h .. + 15]
-  auto aload = [&](const uint32_t (&o)[2], int s, v4i (&x)[2][2]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh) x[t][kh] = *reinterpret_cast<const v4i*>(A + (o[t] + (uint32_t)(64 * s + 32 * kh)));
+    for (int t = 0; t < 2; ++t) o[t] = __builtin_amdgcn_readfirstlane((uint32_t)(2 * i + t) * kb32 * 1024u);
   };
   const int8_t* wlane = wl + lane * 16;
   auto wload = [&](int s, v4i (&w)[NTN][2]) __attribute__((always_inline)) {
@@ -183,8 +193,20 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(const int8_t* __restr
   v4i wf[2][NTN][2];
   uint32_t ao[2];
   aoffs(ti, ao);
+  // (t, stage, k half) order: one row tile's accesses to the same lines are adjacent
+  auto agroup = [&](const uint32_t (&o)[2], int s0, int slot0) __attribute__((always_inline)) {
 #pragma unroll
-  for (int s = 0; s < PD; ++s) aload(ao, s, xs[s]);
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int g = 0; g < GS; ++g)
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+          xs[slot0 + g][t][kh] =
+              *reinterpret_cast<const v4i*>(A + o[t] + (uint32_t)((2 * (s0 + g) + kh) * 1024) + lane16);
+  };
+  static_assert(NKC % GS == 0 && PD % GS == 0, "stage groups");
+#pragma unroll
+  for (int s = 0; s < PD; s += GS) agroup(ao, s, s);
   auto tile = [&](int i, int inext) __attribute__((always_inline)) {
     WS_STAMP(st_a);
     uint32_t an[2];
@@ -192,9 +214,11 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(const int8_t* __restr
     wload(0, wf[0]);
 #pragma unroll
     for (int s = 0; s < NKC; ++s) {
-      // stage s + PD (past the tile's end: the next tile's first stages)
-      if (s + PD < NKC) aload(ao, s + PD, xs[s + PD]);
-      else aload(an, s + PD - NKC, xs[s + PD]);
+      // stages s + PD .. + GS - 1 (past the tile's end: the next tile's first stages)
+      if (s % GS == 0) {
+        if (s + PD < NKC) agroup(ao, s + PD, s + PD);
+        else agroup(an, s + PD - NKC, s + PD);
+      }
       if (s + 1 < NKC) wload(s + 1, wf[(s + 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
       const v4i(&x)[2][2] = xs[s];
@@ -301,17 +325,17 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(const int8_t* __restr
 }
 
 template <int NTN, int NKC>
-int ws_launch(int epi, const int8_t* A, int64_t M, int64_t lda, const void* Wp, int64_t N, void* C, int64_t ldc,
-              const WsArgs& ep, hipStream_t stream) {
+int ws_launch(int epi, const int8_t* A, int64_t M, const void* Wp, int64_t N, void* C, int64_t ldc, const WsArgs& ep,
+              hipStream_t stream) {
   const int panels = (int)(N / (32 * NTN));
   const int8_t* w = reinterpret_cast<const int8_t*>(Wp);
   int8_t* c = reinterpret_cast<int8_t*>(C);
   if (epi == QVIT_EPI_I8_GELU)
-    hipLaunchKernelGGL((gemm_ws_kernel<NTN, NKC, QVIT_EPI_I8_GELU>), dim3(256), dim3(WS_NT), 0, stream, A, (int)M, lda,
-                       w, c, ldc, panels, ep);
+    hipLaunchKernelGGL((gemm_ws_kernel<NTN, NKC, QVIT_EPI_I8_GELU>), dim3(256), dim3(WS_NT), 0, stream, A, (int)M, w, c,
+                       ldc, panels, ep);
   else
-    hipLaunchKernelGGL((gemm_ws_kernel<NTN, NKC, QVIT_EPI_I8>), dim3(256), dim3(WS_NT), 0, stream, A, (int)M, lda, w,
-                       c, ldc, panels, ep);
+    hipLaunchKernelGGL((gemm_ws_kernel<NTN, NKC, QVIT_EPI_I8>), dim3(256), dim3(WS_NT), 0, stream, A, (int)M, w, c,
+                       ldc, panels, ep);
   return qvit_hip_status(hipGetLastError());
 }
 
@@ -327,24 +351,28 @@ extern "C" int qvit_gemm_ws_stamps(unsigned long long* host8, int reset) {
 }
 #endif
 
-// Called by qvit_gemm (gemm_w4a8.hip) for the int8-code epilogues on int4 weights: returns 1 after launching the
-// weight-stationary kernel when the shape fits it, 0 otherwise (the caller then runs gemm_kernel). Shapes: K = 768 or
-// 1024 (the panel's int8 image in LDS), N = npad = 32 panels of 96 or 128 rows (one per CU of an XCD), 16-B aligned
-// code rows. Arguments are already validated by qvit_gemm.
-__attribute__((visibility("hidden"))) int qvit_gemm_ws_try(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int64_t N, int64_t npad,
-                     const float* d_act, const float* d_wt, const float* bias, int epilogue, void* C, int64_t ldc,
-                     int out_qtype, const float* out_d, const float* out_qm, const float* out_t, int out_levels,
-                     const void* epi_table, hipStream_t stream) {
-  if (epilogue != QVIT_EPI_I8 && epilogue != QVIT_EPI_I8_GELU) return 0;
-  if (N != npad || (ldc % 16) || (((uintptr_t)C) & 15) || M <= 0) return 0;
-  if (M * lda + lda > (int64_t)0xFFFFFFFF) return 0;  // 32-bit activation offsets
+extern "C" int qvit_gemm_a32_fits(int64_t K, int wfmt, int64_t N, int64_t npad, int epilogue) {
+  if (wfmt != QVIT_W4 || (epilogue != QVIT_EPI_I8 && epilogue != QVIT_EPI_I8_GELU) || N != npad) return 0;
+  return (K == 768 || K == 1024) && N == 32 * 96;
+}
+
+extern "C" int qvit_gemm_a32(const int8_t* A, int64_t M, int64_t K, const void* Wp, int wfmt, int64_t N, int64_t npad,
+                             const float* d_act, const float* d_wt, const float* bias, int epilogue, void* C,
+                             int64_t ldc, int out_qtype, const float* out_d, const float* out_qm, const float* out_t,
+                             int out_levels, const void* epi_table, hipStream_t stream) {
+  if (!A || !Wp || !C || !d_act || !d_wt) return QVIT_ENULL;
+  if (!qvit_gemm_a32_fits(K, wfmt, N, npad, epilogue)) return QVIT_EINVAL;
+  if (M < 0 || M > INT32_MAX / 2 || ldc < N) return QVIT_EINVAL;
+  if ((M + 63) / 64 * 64 * K > (int64_t)0xFFFFFFFF) return QVIT_EINVAL;  // 32-bit activation offsets
+  const int q = out_qtype & 0xff;
+  if (q != QVIT_QT_LINEAR && q != QVIT_QT_NONLINEAR && q != QVIT_QT_ULTRA_ACT) return QVIT_EINVAL;
+  if (q == QVIT_QT_ULTRA_ACT ? (out_levels < 1 || out_levels > 127) : (!out_d || !out_qm)) return QVIT_EINVAL;
+  if ((((uintptr_t)A) & 15) || (((uintptr_t)Wp) & 15) || (ldc % 16) || (((uintptr_t)C) & 15)) return QVIT_EALIGN;
+  if ((bias && (((uintptr_t)bias) & 15)) || (epi_table && (((uintptr_t)epi_table) & 15))) return QVIT_EALIGN;
+  if (M == 0) return QVIT_OK;
   const WsArgs ep{d_act, d_wt, bias, out_qtype, out_d, out_qm, out_t, out_levels,
                   reinterpret_cast<const int8_t*>(epi_table)};
-  int rc = -1;
-  if (N == 32 * 96) {
-    if (K == 768) rc = ws_launch<3, 12>(epilogue, A, M, lda, Wp, N, C, ldc, ep, stream);
-    else if (K == 1024) rc = ws_launch<3, 16>(epilogue, A, M, lda, Wp, N, C, ldc, ep, stream);
-  }  // (128-row panels, N = 4096: the accumulators and the two weight-fragment buffers exceed the register budget)
-  if (rc == -1) return 0;
-  return rc == QVIT_OK ? 1 : rc;
+  const int8_t* a = reinterpret_cast<const int8_t*>(A);
+  if (K == 768) return ws_launch<3, 12>(epilogue, a, M, Wp, N, C, ldc, ep, stream);
+  return ws_launch<3, 16>(epilogue, a, M, Wp, N, C, ldc, ep, stream);
 }

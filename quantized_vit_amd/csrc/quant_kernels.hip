@@ -300,7 +300,13 @@ __global__ __launch_bounds__(kThreads) void layernorm_quant_reg_kernel(
 // gamma/beta, the quantizer scalars and the code table (QVIT_EPI_I8 semantics, nullable) are read once
 // per workgroup. Same arithmetic as layernorm_quant_reg_kernel, row for row.
 constexpr int LN_TBL_BYTES = 16384;
-template <int NV>
+// T32: codes in the 32x32x32 MFMA operand order of qvit_gemm_a32 (QVIT_ACT_T32): column c of row r at
+// ((r >> 5) (kpad >> 5) + (c >> 5)) * 1024 + ((r & 31) + 32 ((c >> 4) & 1)) * 16 + (c & 15); a lane's 4-code word
+// stays 4 contiguous bytes (4 | c)
+QVIT_DEV int64_t t32_offset(int64_t r, int64_t c, int64_t kpad) {
+  return ((r >> 5) * (kpad >> 5) + (c >> 5)) * 1024 + ((r & 31) + 32 * ((c >> 4) & 1)) * 16 + (c & 15);
+}
+template <int NV, bool T32 = false>
 __global__ __launch_bounds__(kThreads, 1) void layernorm_quant_persist_kernel(
     const float* __restrict__ x, int64_t rows, int64_t cols, int64_t ldx, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, int qtype, const float* d, const float* qm, const float* t,
@@ -353,13 +359,22 @@ __global__ __launch_bounds__(kThreads, 1) void layernorm_quant_persist_kernel(
                        bv = gbl[256 + lane + 64 * i];
                      },
                      ent, c0, inv_w, top, p, word);
-    int8_t* cr = codes + r * ldc;
+    if constexpr (T32) {
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int64_t c = 4 * (lane + 64 * i);
-      if (c < cols) *reinterpret_cast<uint32_t*>(cr + c) = word[i];
+      for (int i = 0; i < NV; ++i) {
+        const int64_t c = 4 * (lane + 64 * i);
+        if (c < cols) *reinterpret_cast<uint32_t*>(codes + t32_offset(r, c, kpad)) = word[i];
+      }
+      for (int64_t c = cols + lane; c < kpad; c += 64) codes[t32_offset(r, c, kpad)] = 0;
+    } else {
+      int8_t* cr = codes + r * ldc;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int64_t c = 4 * (lane + 64 * i);
+        if (c < cols) *reinterpret_cast<uint32_t*>(cr + c) = word[i];
+      }
+      for (int64_t c = cols + lane; c < kpad; c += 64) cr[c] = 0;
     }
-    for (int64_t c = cols + lane; c < kpad; c += 64) cr[c] = 0;
 #pragma unroll
     for (int i = 0; i < NV; ++i) v[i] = vn[i];
   }
@@ -579,6 +594,48 @@ int qvit_layernorm_quant_i8(const float* x, int64_t rows, int64_t cols, int64_t 
     hipLaunchKernelGGL(layernorm_quant_kernel, dim3(grid_for(rows * 64, kThreads)), dim3(kThreads), 0, stream, x,
                        rows, cols, ldx, gamma, beta, eps, qtype, d_quant, q_m, t_quant, levels, codes, ldc, kpad);
 #undef QVIT_LN_REG
+  return qvit_hip_status(hipGetLastError());
+}
+
+int qvit_layernorm_quant_i8_t32(const float* x, int64_t rows, int64_t cols, int64_t ldx, const float* gamma,
+                                const float* beta, float eps, int qtype, const float* d_quant, const float* q_m,
+                                const float* t_quant, int levels, int8_t* codes, int64_t kpad, const void* code_table,
+                                hipStream_t stream) {
+  if (!x || !codes) return QVIT_ENULL;
+  if (code_table && (((uintptr_t)code_table) & 15)) return QVIT_EALIGN;
+  if (!qtype_ok(qtype) || !qptrs_ok(qtype, d_quant, q_m, levels)) return QVIT_EINVAL;
+  if (rows < 0 || cols <= 0 || cols > 1024 || (cols & 3) || ldx < cols || kpad < cols || (kpad & 63)) return QVIT_EINVAL;
+  if ((ldx & 3) || (((uintptr_t)x) & 15) || (gamma && (((uintptr_t)gamma) & 15)) || (beta && (((uintptr_t)beta) & 15)) ||
+      (((uintptr_t)codes) & 15))
+    return QVIT_EALIGN;
+  if (rows == 0) return QVIT_OK;
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess || n <= 0)
+      n = 256;
+    return n;
+  }();
+  auto resident = [](const void* fn) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kThreads, 0) != hipSuccess || n <= 0) n = 4;
+    return std::min(n, 8);
+  };
+  const int8_t* tab = reinterpret_cast<const int8_t*>(code_table);
+  const int nv = (int)((cols + 255) / 256);
+#define QVIT_LN_T(NV)                                                                                             \
+  do {                                                                                                            \
+    static const int per_cu = resident(reinterpret_cast<const void*>(&layernorm_quant_persist_kernel<NV, true>)); \
+    const int64_t pg = std::min<int64_t>((rows + 3) / 4, (int64_t)per_cu * cus);                                  \
+    hipLaunchKernelGGL((layernorm_quant_persist_kernel<NV, true>), dim3((unsigned)pg), dim3(kThreads), 0, stream,  \
+                       x, rows, cols, ldx, gamma, beta, eps, qtype, d_quant, q_m, t_quant, levels, codes, kpad,    \
+                       kpad, tab);                                                                                \
+  } while (0)
+  if (nv <= 1) QVIT_LN_T(1);
+  else if (nv <= 2) QVIT_LN_T(2);
+  else if (nv <= 3) QVIT_LN_T(3);
+  else QVIT_LN_T(4);
+#undef QVIT_LN_T
   return qvit_hip_status(hipGetLastError());
 }
 

@@ -441,6 +441,20 @@ class QuantizeMixin:
                   plan.bias_pad, epilogue, out, **oq)
         return out
 
+    def a32_fits(self, plan: QuantPlan, epilogue: int) -> bool:
+        """Whether gemm_codes_a32 runs this layer (qvit_gemm_a32_fits: the fc1 shape class)."""
+        return _lib.gemm_a32_fits(plan.kpad, plan.wfmt, plan.n, plan.npad, epilogue)
+
+    def gemm_codes_a32(self, codes_t32: torch.Tensor, M: int, plan: QuantPlan, epilogue: int, out: torch.Tensor,
+                       next_layer: "QuantizeMixin") -> torch.Tensor:
+        """gemm_codes for the int8-code epilogues on QVIT_ACT_T32 activation codes (qvit_gemm_a32: weight-stationary
+        schedule, same codes as gemm_codes on the row-major codes)."""
+        nplan = next_layer.quant_plan()
+        _lib.gemm_a32(codes_t32, M, plan.kpad, plan.packed, plan.wfmt, plan.n, plan.npad, plan.d_act, plan.d_wt,
+                      plan.bias_pad, epilogue, out, out_qtype=nplan.qtype, out_d=nplan.d_act, out_qm=nplan.qm_act,
+                      out_t=nplan.t_act, epi_table=epilogue_table(nplan, epilogue))
+        return out
+
 
 _GELU_MAX_SLOPE = 1.1289   # max of d/dv [v Phi(v)] (at v ~ 1.41)
 

@@ -28,6 +28,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
+from . import quant_layers as _ql
 from .quant_layers import QuantizationMode, QuantizeConv2d, QuantizeLinear, epilogue_table, trace_codes
 
 # The residual GEMMs (proj, fc2) run the following LayerNorm + quantizer behind their tiles (qvit_gemm_resid_ln)
@@ -344,6 +345,23 @@ class Block(nn.Module):
         Returns (x, next_block's norm1 codes when fc2 produced them, else None)."""
         m = self.mlp
         p_fc1 = m.fc1.quant_plan()
+        p_fc2 = m.fc2.quant_plan()
+        hid = torch.empty((M, p_fc2.kpad), dtype=torch.int8, device=x.device)
+        if p_fc2.kpad != p_fc1.n:
+            hid[:, p_fc1.n:].zero_()
+        if codes_in is None and m.fc1.a32_fits(p_fc1, _lib.EPI_I8_GELU) and self.norm2.weight.is_contiguous():
+            # norm2's codes in the MFMA operand order of the weight-stationary fc1 (qvit_gemm_a32): every fragment
+            # load of the GEMM one contiguous KiB
+            codes = torch.empty(_lib.t32_rows(M) * p_fc1.kpad, dtype=torch.int8, device=x.device)
+            with _timed("ln"):
+                _lib.layernorm_quant_i8_t32(x2, self.norm2.weight, self.norm2.bias, self.norm2.eps, p_fc1.qtype,
+                                            p_fc1.d_act, p_fc1.qm_act, p_fc1.t_act, 0, codes, p_fc1.kpad,
+                                            code_table=epilogue_table(p_fc1, _lib.EPI_I8))
+            if _ql.CODE_TRACE is not None:
+                trace_codes(m.fc1, _lib.t32_to_rows(codes, M, p_fc1.kpad), p_fc1.k)
+            with _timed("fc1"):
+                m.fc1.gemm_codes_a32(codes, M, p_fc1, _lib.EPI_I8_GELU, hid, m.fc2)
+            return self._fc2_fused_(x, x2, hid, p_fc2, next_block)
         if codes_in is not None:
             codes = codes_in
         else:
@@ -353,12 +371,13 @@ class Block(nn.Module):
                                         p_fc1.d_act, p_fc1.qm_act, p_fc1.t_act, 0, codes, p_fc1.kpad,
                                         code_table=epilogue_table(p_fc1, _lib.EPI_I8))
         trace_codes(m.fc1, codes, p_fc1.k)
-        p_fc2 = m.fc2.quant_plan()
-        hid = torch.empty((M, p_fc2.kpad), dtype=torch.int8, device=x.device)
-        if p_fc2.kpad != p_fc1.n:
-            hid[:, p_fc1.n:].zero_()
         with _timed("fc1"):
             m.fc1.gemm_codes(codes, p_fc1, _lib.EPI_I8_GELU, out=hid, next_layer=m.fc2)
+        return self._fc2_fused_(x, x2, hid, p_fc2, next_block)
+
+    def _fc2_fused_(self, x: torch.Tensor, x2: torch.Tensor, hid: torch.Tensor, p_fc2: QuantPlan,
+                    next_block: Optional["Block"] = None):
+        m = self.mlp
         trace_codes(m.fc2, hid, p_fc2.k)
         if next_block is not None and self.ln_fusable(x2, next_block.norm1, p_fc2):
             with _timed("fc2"):

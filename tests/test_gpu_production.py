@@ -139,9 +139,19 @@ def test_gemm_resid_ln_shapes(dev, M, N, K, qt, table):
     _resid_ln_case(dev, M, N, K, seed=M + N, qt=qt, table=table)
 
 
+def _gemm_fc1(A, M, kpad, packed, npad, N, d_a, d_w, bias_pad, out, path, **kw):
+    if path == "a32":  # the weight-stationary schedule on T32 codes (the fused block's fc1)
+        _lib.gemm_a32(_lib.rows_to_t32(A, kpad), M, kpad, packed, _lib.W4, N, npad, d_a, d_w, bias_pad,
+                      _lib.EPI_I8_GELU, out, **kw)
+    else:
+        _lib.gemm(A, M, kpad, packed, _lib.W4, N, npad, d_a, d_w, bias_pad, _lib.EPI_I8_GELU, out, **kw)
+
+
+@pytest.mark.parametrize("path", ["tiles", "a32"])
 @pytest.mark.parametrize("qt,t", [(O.NONLINEAR, 1.0), (O.LINEAR, 1.0)])
-def test_gemm_b256_gelu_code_epilogue(dev, qt, t):
-    """fc1: d_a d_w acc + b -> GELU -> fc2's quantizer via the code table, int8 out (4 728 tiles)."""
+def test_gemm_b256_gelu_code_epilogue(dev, qt, t, path):
+    """fc1: d_a d_w acc + b -> GELU -> fc2's quantizer via the code table, int8 out (4 728 tiles of the persistent
+    schedule, or 788 wave tiles of the weight-stationary one on T32 codes: path a32)."""
     from quantized_vit_amd.quant_layers import epilogue_table_geometry, saturation_level
     N, K = 3072, 768
     assert _tiles(M256, N) > 2 * BLOCKS_PER_CU * _cus(dev)
@@ -159,8 +169,7 @@ def test_gemm_b256_gelu_code_epilogue(dev, qt, t):
     outs = []
     for tab in (table, None):
         out = torch.full((M256, N), 99, dtype=torch.int8, device=dev)
-        _lib.gemm(A, M256, kpad, packed, _lib.W4, N, npad, _p(d_a, dev), _p(d_w, dev), bias_pad, _lib.EPI_I8_GELU,
-                  out, epi_table=tab, **kw)
+        _gemm_fc1(A, M256, kpad, packed, npad, N, _p(d_a, dev), _p(d_w, dev), bias_pad, out, path, epi_table=tab, **kw)
         outs.append(out.cpu())
     assert int(table[12:16].view(torch.int32).item()) == 1
     # the table re-expresses the per-element evaluation (same kernel, same cross-tile schedule)

@@ -24,6 +24,7 @@ SHAPES = {
     "qkv": (M_B256, 2304, 768, _lib.EPI_F32),
     "proj": (M_B256, 768, 768, _lib.EPI_F32_RESID),
     "fc1": (M_B256, 3072, 768, _lib.EPI_I8_GELU),
+    "fc1_a32": (M_B256, 3072, 768, _lib.EPI_I8_GELU),   # qvit_gemm_a32 on T32 codes (the fused block's fc1)
     "fc1_f32": (M_B256, 3072, 768, _lib.EPI_F32),
     "fc1_i32": (M_B256, 3072, 768, _lib.EPI_I32),
     "fc1_i8": (M_B256, 3072, 768, _lib.EPI_I8),
@@ -66,10 +67,14 @@ def run(name, M, N, K, epi, iters, dev, qtype=_lib.QT_NONLINEAR):
         geo = epilogue_table_geometry(qtype, 4.0 / 127, 4.0, 1.0, saturation_level(qtype, 4.0 / 127, 4.0, 1.0), False)
         tab = _lib.epi_table_build(_lib.EPI_I8, qtype, kw["out_d"], kw["out_qm"], kw["out_t"], 0, *geo, dev)
 
+    A32 = _lib.rows_to_t32(A, K) if name.endswith("a32") else None
+
     def launch():
         if epi == -1:
             _lib.gemm_resid_ln(A, M, K, packed, _lib.W4, N, npad, d_a, d_w, bias, C, gamma, beta, 1e-6, qtype,
                                kw["out_d"], kw["out_qm"], kw["out_t"], 0, tab, codes, N)
+        elif name.endswith("a32"):
+            _lib.gemm_a32(A32, M, K, packed, _lib.W4, N, npad, d_a, d_w, bias, epi, C, **kw)
         else:
             _lib.gemm(A, M, K, packed, _lib.W4, N, npad, d_a, d_w, bias, epi, C, **kw)
     times = []
