@@ -67,6 +67,15 @@ DRYRUN = os.environ.get("QVIT_BENCH_DRYRUN") == "1"
 ONE_DEVICE = os.environ.get("QVIT_BENCH_ONE_DEVICE") == "1"
 
 
+def _step_marker() -> None:
+    """With QVIT_STEP_MARKERS=1 (profiling runs only): one tiny torch spin kernel just before and just after the
+    timed steps, OUTSIDE the timed region, so tools/kstats.py --split can tell the timed steps' dispatches in a
+    rocprofv3 kernel trace from setup, calibration, event-timed and parity launches."""
+    if os.environ.get("QVIT_STEP_MARKERS") == "1":
+        torch.cuda._sleep(64)
+        torch.cuda.synchronize()
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -187,7 +196,9 @@ def parity_report(model, model_name: str, img_size: int, dev) -> dict:
       `rel_device_weights` (the timed configuration: the device's own weight codes), `weight_code_flips` (device
       weight codes that differ from the oracle's, and how many of those the correctly rounded quantizer
       explains, oracle/ties.py:cr_codes), `rel_oracle_weights` (the oracle's weight codes bound: what remains is
-      the activation codes' contribution), `floor_fp32_vs_fp64` (the oracle against itself in fp64).
+      the activation codes' contribution), `floor_fp32_vs_fp64` (the oracle against itself in fp64), and
+      `default_gelu`: the same distances to the oracle run with torch's default (oneDNN) GELU instead of the pinned
+      ATen kernel — what a default-configured reference would see (reported; not a criterion).
     * `tie_resolved`: with the oracle's weight codes bound, every quantizer boundary of the GPU forward against
       the oracle's (oracle/ties.py). A differing code must be a proven rounding tie, and no layer may flip more
       than the tests' 1e-4 budget of its codes; with ties resolved alike `rel` is the logits' distance. `pass`
@@ -225,8 +236,13 @@ def parity_report(model, model_name: str, img_size: int, dev) -> dict:
                 wlayers[name] = {"flips": n, "cr_explained": c}
         load_oracle_weight_codes(model, cfg)
         y_ow = model(img.to(dev)).cpu()
+        with O.torch_default_gelu():
+            ref_def = O.vit_forward(sd, cfg, img)
     untied = {"rel_device_weights": rel(y_dev, ref), "rel_oracle_weights": rel(y_ow, ref),
               "floor_fp32_vs_fp64": rel(ref, ref64),
+              # reported, not a criterion: against a reference run in torch's default configuration (oneDNN GELU)
+              "default_gelu": {"rel_device_weights": rel(y_dev, ref_def), "rel_oracle_weights": rel(y_ow, ref_def),
+                               "oracle_pinned_vs_default": rel(ref, ref_def)},
               "weight_code_flips": {"flips": wflips, "cr_explained": wcr, "codes": wtot, "layers": wlayers}}
     r = tie_resolved_vit_check(model, cfg, img, dev)
     non_ties = sum(s.get("non_ties", 0) for s in r["stats"].values())
@@ -352,6 +368,7 @@ def main():
         assert out.shape == (global_batch, model.head.out_features), out.shape
         # timed region: only the roofline kernel (fc1) carries HIP events
         vit_model.KERNEL_TIMING["fc1"] = []
+        _step_marker()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -362,6 +379,7 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
+        _step_marker()
         events = {"fc1": vit_model.KERNEL_TIMING.pop("fc1")}
         # the other hot kernels: the same steps again with events around each of their launches (untimed)
         for n in names[1:]:
@@ -515,6 +533,7 @@ def ultranet_main(args, world: int, rank: int, dev, backend: str, one_device: bo
         torch.cuda.synchronize()
         assert out.shape[0] == global_batch, out.shape
         vit_model.KERNEL_TIMING["ultra_conv0"] = []
+        _step_marker()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -525,6 +544,7 @@ def ultranet_main(args, world: int, rank: int, dev, backend: str, one_device: bo
             dist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
+        _step_marker()
         events = {"ultra_conv0": vit_model.KERNEL_TIMING.pop("ultra_conv0")}
         for n in names[1:]:
             vit_model.KERNEL_TIMING[n] = []
@@ -545,7 +565,12 @@ def ultranet_main(args, world: int, rank: int, dev, backend: str, one_device: bo
         kernels[n] = {"launch_us": ms * 1e3, "hbm_GBs_algorithmic": w["bytes"] * B / (ms * 1e-3) / 1e9,
                       "int8_TOPS": w["ops"] * B / (ms * 1e-3) / 1e12}
     k0 = kernels["ultra_conv0"]
-    per_layer = [n for n, *_ in ULTRA_LAYERS] + ["ultra_head", "ultra_decode"]   # (the tail fuses 4..7 + head)
+    # the launches that actually ran: with qvit_ultra_tail the layers 4..7, the head and the decode are
+    # one launch moving the tail's own bytes (layer 4's codes in, io and p out), not the per-layer sum
+    if "ultra_tail" in launch_ms:
+        per_layer = [n for n, *_ in ULTRA_LAYERS[:4]] + ["ultra_tail"]
+    else:
+        per_layer = [n for n, *_ in ULTRA_LAYERS] + ["ultra_head", "ultra_decode"]
     img_bytes = sum(work[n]["bytes"] for n in per_layer)
     img_ops = sum(work[n]["ops"] for n in per_layer)
     value = global_batch * args.steps / elapsed
@@ -563,7 +588,7 @@ def ultranet_main(args, world: int, rank: int, dev, backend: str, one_device: bo
                      "achieved": k0["hbm_GBs_algorithmic"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": k0["hbm_GBs_algorithmic"] / HBM_PEAK_GBS, "traffic": None,
                      "bytes_per_launch": work["ultra_conv0"]["bytes"] * B, "launch_ms": launch_ms["ultra_conv0"]},
-        "model_frac": {"algorithmic_bytes_per_img": img_bytes, "int8_ops_per_img": img_ops,
+        "model_frac": {"launches": per_layer, "algorithmic_bytes_per_img": img_bytes, "int8_ops_per_img": img_ops,
                        "hbm_GBs": img_bytes * value / world / 1e9,
                        "frac_hbm_peak": img_bytes * value / world / 1e9 / HBM_PEAK_GBS},
         "kernels": kernels,

@@ -118,6 +118,57 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(const int8_t* __restr
   const int pnl = slot % panels, grp = slot / panels;
   const int n0 = pnl * PW;
 
+  // ---- this wave's 64-row tiles: XCD x owns wave-tiles [xlo, xhi) of ceil(M / 64), its group a contiguous part
+  const int nwt = (M + 63) >> 6;
+  const int xlo = (int)((int64_t)xcd * nwt / 8), xhi = (int)((int64_t)(xcd + 1) * nwt / 8);
+  const int glo = xlo + (int)((int64_t)(xhi - xlo) * grp / groups);
+  const int ghi = xlo + (int)((int64_t)(xhi - xlo) * (grp + 1) / groups);
+  int ti = glo + wave;
+  const bool has_tiles = ti < ghi;  // (waves without a tile still take part in the weight fill)
+
+  const int lane = tid & 63;
+  const int lr = lane & 31, lh = lane >> 5;
+  // T32 activations: the 1-KiB block of rows 32 mb .. + 31, k 32 kb .. + 31 at (mb KB32 + kb) KiB, lane l's 16 B at
+  // 16 l (rows past M exist in the padded buffer: loaded, never stored); per tile one uniform offset
+  const uint32_t kb32 = (uint32_t)(NKC * 2);
+  const uint32_t lane16 = (uint32_t)lane * 16u;
+  auto aoffs = [&](int i, uint32_t (&o)[2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) o[t] = __builtin_amdgcn_readfirstlane((uint32_t)(2 * i + t) * kb32 * 1024u);
+  };
+  const int8_t* wlane = wl + lane * 16;
+  auto wload = [&](int s, v4i (&w)[NTN][2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < NTN; ++u)
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) w[u][kh] = *reinterpret_cast<const v4i*>(wlane + ((s * NTN + u) * 2 + kh) * 1024);
+  };
+
+  v16i acc[2][NTN];
+  // activation stages of a tile (the k-loop is straight-line code, so each stage's fragments are their own values:
+  // three stages live at a time), xs[NKC], xs[NKC + 1] = the next tile's stages 0, 1, carried over
+  v4i xs[NKC + PD][2][2];
+  v4i wf[2][NTN][2];
+  uint32_t ao[2];
+  aoffs(ti, ao);
+  // (t, stage, k half) order: one row tile's accesses to the same lines are adjacent
+  auto agroup = [&](const uint32_t (&o)[2], int s0, int slot0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int g = 0; g < GS; ++g)
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+          xs[slot0 + g][t][kh] =
+              *reinterpret_cast<const v4i*>(A + o[t] + (uint32_t)((2 * (s0 + g) + kh) * 1024) + lane16);
+  };
+  static_assert(NKC % GS == 0 && PD % GS == 0, "stage groups");
+  // the first tile's first stages load while the weights are filled in
+  if (has_tiles) {
+#pragma unroll
+    for (int s = 0; s < PD; s += GS) agroup(ao, s, s);
+  }
+
   // ---- once per launch: the panel's weights (int4 image -> 16x-scaled int8, lane-linear fragments), its bias, the
   // quantizer's code table and scalars
   {
@@ -159,54 +210,8 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(const int8_t* __restr
 #ifdef QVIT_GEMM_WS_STAMPS
   st_fill = __builtin_amdgcn_s_memtime() - st_t0;
 #endif
+  if (!has_tiles) return;
 
-  // ---- this wave's 64-row tiles: XCD x owns wave-tiles [xlo, xhi) of ceil(M / 64), its group a contiguous part
-  const int nwt = (M + 63) >> 6;
-  const int xlo = (int)((int64_t)xcd * nwt / 8), xhi = (int)((int64_t)(xcd + 1) * nwt / 8);
-  const int glo = xlo + (int)((int64_t)(xhi - xlo) * grp / groups);
-  const int ghi = xlo + (int)((int64_t)(xhi - xlo) * (grp + 1) / groups);
-  int ti = glo + wave;
-  if (ti >= ghi) return;
-
-  const int lane = tid & 63;
-  const int lr = lane & 31, lh = lane >> 5;
-  // T32 activations: the 1-KiB block of rows 32 mb .. + 31, k 32 kb .. + 31 at (mb KB32 + kb) KiB, lane l's 16 B at
-  // 16 l (rows past M exist in the padded buffer: loaded, never stored); per tile one uniform offset
-  const uint32_t kb32 = (uint32_t)(NKC * 2);
-  const uint32_t lane16 = (uint32_t)lane * 16u;
-  auto aoffs = [&](int i, uint32_t (&o)[2]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int t = 0; t < 2; ++t) o[t] = __builtin_amdgcn_readfirstlane((uint32_t)(2 * i + t) * kb32 * 1024u);
-  };
-  const int8_t* wlane = wl + lane * 16;
-  auto wload = [&](int s, v4i (&w)[NTN][2]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int u = 0; u < NTN; ++u)
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh) w[u][kh] = *reinterpret_cast<const v4i*>(wlane + ((s * NTN + u) * 2 + kh) * 1024);
-  };
-
-  v16i acc[2][NTN];
-  // activation stages of a tile (the k-loop is straight-line code, so each stage's fragments are their own values:
-  // three stages live at a time), xs[NKC], xs[NKC + 1] = the next tile's stages 0, 1, carried over
-  v4i xs[NKC + PD][2][2];
-  v4i wf[2][NTN][2];
-  uint32_t ao[2];
-  aoffs(ti, ao);
-  // (t, stage, k half) order: one row tile's accesses to the same lines are adjacent
-  auto agroup = [&](const uint32_t (&o)[2], int s0, int slot0) __attribute__((always_inline)) {
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int g = 0; g < GS; ++g)
-#pragma unroll
-        for (int kh = 0; kh < 2; ++kh)
-          xs[slot0 + g][t][kh] =
-              *reinterpret_cast<const v4i*>(A + o[t] + (uint32_t)((2 * (s0 + g) + kh) * 1024) + lane16);
-  };
-  static_assert(NKC % GS == 0 && PD % GS == 0, "stage groups");
-#pragma unroll
-  for (int s = 0; s < PD; s += GS) agroup(ao, s, s);
   auto tile = [&](int i, int inext) __attribute__((always_inline)) {
     WS_STAMP(st_a);
     uint32_t an[2];
@@ -245,55 +250,70 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(const int8_t* __restr
     // ---- epilogue: lane (token 64 i + 32 t + lr, h) holds columns n0 + 32 u + 16 h .. + 15 of acc[t][u]
     WS_STAMP(st_b);
     __builtin_amdgcn_s_setprio(1);
+    auto store16 = [&](int t, int u, const uint32_t (&wd)[4]) __attribute__((always_inline)) {
+      const int m = 64 * i + 32 * t + lr;
+      if (m < M) *reinterpret_cast<uint4*>(C + (int64_t)m * ldc + n0 + 32 * u + 16 * lh) = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+    };
+    if (use_table) {
+      // the 2 NTN groups g = (u, t) of 16 codes, software-pipelined: group g + 1's 16 table lookups are issued
+      // before group g's selects and store, so each group's LDS latency runs under the previous group's VALU
+      const int8_t* ent = tbl + sizeof(EpiTableHdr);
+      float v[2][16];
+      uint2 e[2][16];
+      auto look = [&](int g, int b) __attribute__((always_inline)) {
+        const int u = g >> 1, t = g & 1;
 #pragma unroll
-    for (int u = 0; u < NTN; ++u) {
-      float bcol[16];
+        for (int q = 0; q < 4; ++q) {
+          const float4 bq = *reinterpret_cast<const float4*>(bias_l + 32 * u + 16 * lh + 4 * q);
+          const float bb[4] = {bq.x, bq.y, bq.z, bq.w};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 b = *reinterpret_cast<const float4*>(bias_l + 32 * u + 16 * lh + 4 * q);
-        bcol[4 * q] = b.x; bcol[4 * q + 1] = b.y; bcol[4 * q + 2] = b.z; bcol[4 * q + 3] = b.w;
-      }
+          for (int j = 0; j < 4; ++j) {
+            v[b][4 * q + j] = fmaf(alpha, (float)acc[t][u][4 * q + j], bb[j]);
+            e[b][4 * q + j] = *epi_entry(ent, v[b][4 * q + j], t_c0, t_invw, t_top);
+          }
+        }
+      };
+      look(0, 0);
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int m = 64 * i + 32 * t + lr;
+      for (int g = 0; g < 2 * NTN; ++g) {
+        if (g + 1 < 2 * NTN) look(g + 1, (g + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
+        const int b = g & 1;
         uint32_t wd[4];
-        if (use_table) {
-          const int8_t* ent = tbl + sizeof(EpiTableHdr);
-          float v[16];
-          uint2 e[16];
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            v[r] = fmaf(alpha, (float)acc[t][u][r], bcol[r]);
-            e[r] = *epi_entry(ent, v[r], t_c0, t_invw, t_top);
-          }
-          __builtin_amdgcn_sched_barrier(0);
+        for (int q = 0; q < 4; ++q) {
+          epi_select_byte<0>(wd[q], v[b][4 * q], __uint_as_float(e[b][4 * q].x), e[b][4 * q].y);
+          epi_select_byte<1>(wd[q], v[b][4 * q + 1], __uint_as_float(e[b][4 * q + 1].x), e[b][4 * q + 1].y);
+          epi_select_byte<2>(wd[q], v[b][4 * q + 2], __uint_as_float(e[b][4 * q + 2].x), e[b][4 * q + 2].y);
+          epi_select_byte<3>(wd[q], v[b][4 * q + 3], __uint_as_float(e[b][4 * q + 3].x), e[b][4 * q + 3].y);
+        }
+        store16(g & 1, g >> 1, wd);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {  // no valid table: the per-element quantizer (rare; same function as gemm_kernel's staged path)
+      const QParams qp = *qp_l;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            epi_select_byte<0>(wd[q], v[4 * q], __uint_as_float(e[4 * q].x), e[4 * q].y);
-            epi_select_byte<1>(wd[q], v[4 * q + 1], __uint_as_float(e[4 * q + 1].x), e[4 * q + 1].y);
-            epi_select_byte<2>(wd[q], v[4 * q + 2], __uint_as_float(e[4 * q + 2].x), e[4 * q + 2].y);
-            epi_select_byte<3>(wd[q], v[4 * q + 3], __uint_as_float(e[4 * q + 3].x), e[4 * q + 3].y);
-          }
-        } else {  // no valid table: the per-element quantizer (rare; same function as gemm_kernel's staged path)
-          const QParams qp = *qp_l;
+      for (int u = 0; u < NTN; ++u)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          uint32_t wd[4];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             float k[4];
             bool need[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-              float v = fmaf(alpha, (float)acc[t][u][4 * q + j], bcol[4 * q + j]);
-              if (EPI == QVIT_EPI_I8_GELU) v = gelu_ref(v);
-              k[j] = quant_fast(v, qp, need[j]);
-              if (need[j]) k[j] = quant_fixup(v, qp);
+              float vv = fmaf(alpha, (float)acc[t][u][4 * q + j], bias_l[32 * u + 16 * lh + 4 * q + j]);
+              if (EPI == QVIT_EPI_I8_GELU) vv = gelu_ref(vv);
+              k[j] = quant_fast(vv, qp, need[j]);
+              if (need[j]) k[j] = quant_fixup(vv, qp);
             }
             wd[q] = 0;
 #pragma unroll
             for (int j = 0; j < 4; ++j) wd[q] |= ((uint32_t)(uint8_t)to_i8_sat(k[j])) << (8 * j);
           }
+          store16(t, u, wd);
         }
-        if (m < M) *reinterpret_cast<uint4*>(C + (int64_t)m * ldc + n0 + 32 * u + 16 * lh) = make_uint4(wd[0], wd[1], wd[2], wd[3]);
-      }
     }
     __builtin_amdgcn_s_setprio(0);
 #ifdef QVIT_GEMM_WS_STAMPS

@@ -134,6 +134,12 @@ def _codes_path(w_bit: int) -> bool:
     return 2 <= w_bit <= 8
 
 
+def _needs_grad(module: nn.Module, input: torch.Tensor) -> bool:
+    """Autograd wants this call's history: the packed-codes kernels record none, so such calls take the
+    reference's own F.conv2d / F.linear on quantize_fn(weight) (quant_ultra.py:85-89, :219-222), gradients included."""
+    return torch.is_grad_enabled() and (input.requires_grad or any(p.requires_grad for p in module.parameters()))
+
+
 def conv2d_Q_fn(w_bit):
     """quant_ultra.py:76-91."""
 
@@ -151,11 +157,17 @@ def conv2d_Q_fn(w_bit):
                 self._codes.get(self.weight, self.bias, self.w_bit)
             return self
 
+        def invalidate(self):
+            """Drops the packed codes: needed only after editing the weight or bias through `.data` (which bypasses the
+            version counter the cache keys on; QuantizeMixin.invalidate alike)."""
+            self._codes.key = None
+            return self
+
         def forward(self, input, order=None):
             if _codes_path(self.w_bit):
                 _check_gpu(input, "input")
             if _codes_path(self.w_bit) and self.groups == 1 and self.padding_mode == "zeros" and \
-                    not isinstance(self.padding, str) and input.dim() == 4:
+                    not isinstance(self.padding, str) and input.dim() == 4 and not _needs_grad(self, input):
                 c = self._codes.get(self.weight, self.bias, self.w_bit)
                 return _lib.conv_wonly(input.detach(), self.kernel_size, self.stride, self.padding, self.dilation,
                                        c.packed, c.wfmt, c.n, c.npad, c.kpad, c.d_wt, c.bias_pad)
@@ -224,8 +236,13 @@ def linear_Q_fn(w_bit):
                 self._codes.get(self.weight, self.bias, self.w_bit)
             return self
 
+        def invalidate(self):
+            """Drops the packed codes (see Conv2d_Q.invalidate)."""
+            self._codes.key = None
+            return self
+
         def forward(self, input):
-            if not _codes_path(self.w_bit):
+            if not _codes_path(self.w_bit) or _needs_grad(self, input):
                 return F.linear(input, self.quantize_fn(self.weight), self.bias)
             _check_gpu(input, "input")
             c = self._codes.get(self.weight, self.bias, self.w_bit)

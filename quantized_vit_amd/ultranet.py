@@ -215,7 +215,9 @@ class UltraNetQua(nn.Module):
     def forward_modules(self, x):
         """mymodel.py:134-144 module by module: Conv2d_Q on qvit_conv_wonly, activation_quantize_fn on the HIP
         quantizer; BatchNorm2d and MaxPool2d on ATen's own kernels (the MIOpen batch-norm route off, so no
-        library kernel is on the path). Any image size, training mode included."""
+        library kernel is on the path). Any image size, training mode included; under autograd (grad mode on and a
+        parameter or the input requiring grad) the Conv2d_Q layers take the reference's F.conv2d on the fake-quant
+        weight instead, so gradients flow (the packed-codes kernels record no history)."""
         img_size = x.shape[-2:]
         yolo_out = []
         with _aten_batch_norm():

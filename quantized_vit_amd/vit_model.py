@@ -36,6 +36,11 @@ from .quant_layers import QuantizationMode, QuantizeConv2d, QuantizeLinear, epil
 # form is bit-identical but measured slower (the LayerNorm of a 128-row block
 # runs on the one workgroup that completes the block and stalls its tile pipeline).
 FUSE_RESID_LN = os.environ.get("QVIT_FUSE_LN", "0") == "1"
+# fc1 on the weight-stationary schedule (norm2 writes QVIT_ACT_T32 codes, qvit_gemm_a32) instead of the tile
+# schedule when QVIT_FC1_A32=1 (or FC1_WEIGHT_STATIONARY = True). Off by default: bit-identical, faster on
+# full-range random codes but 2-3 % slower on the model's own activations, and its LayerNorm 4 % slower
+# (profiles/r05_fc1_weight_stationary_ab.txt).
+FC1_WEIGHT_STATIONARY = os.environ.get("QVIT_FC1_A32", "0") == "1"
 
 # Benchmark instrumentation: when KERNEL_TIMING[name] is a list (name in "fc1", "fc2", "proj",
 # "qkv_attn", "ln"), the fused block appends a (start, end) HIP event pair recorded on the launch
@@ -349,7 +354,8 @@ class Block(nn.Module):
         hid = torch.empty((M, p_fc2.kpad), dtype=torch.int8, device=x.device)
         if p_fc2.kpad != p_fc1.n:
             hid[:, p_fc1.n:].zero_()
-        if codes_in is None and m.fc1.a32_fits(p_fc1, _lib.EPI_I8_GELU) and self.norm2.weight.is_contiguous():
+        if (FC1_WEIGHT_STATIONARY and codes_in is None and m.fc1.a32_fits(p_fc1, _lib.EPI_I8_GELU)
+                and self.norm2.weight.is_contiguous()):
             # norm2's codes in the MFMA operand order of the weight-stationary fc1 (qvit_gemm_a32): every fragment
             # load of the GEMM one contiguous KiB
             codes = torch.empty(_lib.t32_rows(M) * p_fc1.kpad, dtype=torch.int8, device=x.device)

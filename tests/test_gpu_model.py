@@ -290,6 +290,25 @@ def test_vit_resid_ln_fusion_bit_identical(dev, name, depth, batch):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("batch", [1, 5])
+def test_vit_fc1_weight_stationary_bit_identical(dev, batch):
+    """fc1 on the weight-stationary schedule (norm2 -> QVIT_ACT_T32 codes -> qvit_gemm_a32, the opt-in
+    FC1_WEIGHT_STATIONARY route) gives the very same logits as the tile schedule."""
+    model = build_quantized_vit("vit_base_patch16_224", seed=7, depth=2).to(dev)
+    img = synthetic_images(batch, 224, seed=3).to(dev)
+    assert model.blocks[0].mlp.fc1.a32_fits(model.blocks[0].mlp.fc1.quant_plan(), _lib.EPI_I8_GELU)
+    outs = []
+    saved = vit_model.FC1_WEIGHT_STATIONARY
+    for ws in (True, False):
+        vit_model.FC1_WEIGHT_STATIONARY = ws
+        try:
+            with torch.no_grad():
+                outs.append(model(img).cpu())
+        finally:
+            vit_model.FC1_WEIGHT_STATIONARY = saved
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_vit_linear_quantizer_vs_oracle(dev):
     model = build_quantized_vit("vit_tiny_patch16_224", seed=5, quant_type=QuantizationType.SYMMETRIC_LINEAR).to(dev)
     cfg = O.ViTConfig(embed_dim=192, depth=12, num_heads=3, quant_type=O.LINEAR)

@@ -232,3 +232,22 @@ def test_prepare_packs_before_the_first_forward(dev):
     with torch.no_grad():
         conv(torch.rand(1, 8, 10, 10, device=dev))
     assert conv._codes.key == key
+
+
+def test_conv2d_q_invalidate_and_grad(dev):
+    """a .data edit is picked up after invalidate() (the packed codes key on the version counter, which
+    .data bypasses), and under autograd the module takes the reference's F.conv2d so the input gradient flows."""
+    g = torch.Generator().manual_seed(3)
+    conv = conv2d_Q_fn(4)(16, 32, kernel_size=3, stride=1, padding=1, bias=False).to(dev)
+    x = (torch.randint(0, 16, (1, 16, 20, 20), generator=g).float() / 15.0).to(dev)
+    with torch.no_grad():
+        y0 = conv(x)
+        conv.weight.data.mul_(-1.0)      # bypasses the version counter: the cached codes are now stale ...
+        stale = conv(x)
+        conv.invalidate()                # ... until invalidated
+        y1 = conv(x)
+    assert torch.equal(stale, y0)
+    torch.testing.assert_close(y1, -y0, rtol=0, atol=1e-5)
+    xg = x.clone().requires_grad_(True)
+    conv(xg).sum().backward()             # grad mode: F.conv2d on quantize_fn(weight)
+    assert xg.grad is not None and xg.grad.abs().sum().item() > 0

@@ -1,6 +1,10 @@
 """rocprofv3 summaries.
 
     python tools/kstats.py STATS_CSV [N]                 top kernels of a --stats kernel_stats.csv
+    python tools/kstats.py --split TRACE_CSV STEPS [N]   the same from a --kernel-trace kernel_trace.csv, split into
+                                                        the timed steps' kernels and setup/parity kernels (needs a
+                                                        bench.py run with QVIT_STEP_MARKERS=1: its two spin kernels
+                                                        bracket the timed steps)
     python tools/kstats.py --pmc FETCH_DIR WRITE_DIR [--round r01]
                                                         fc1 HBM traffic per launch from two PMC passes
 
@@ -31,6 +35,51 @@ def top(path, n=25):
             short = name[:40]
         print(f'{float(r["TotalDurationNs"])/1e6:9.3f} ms  calls={int(r["Calls"]):5d}  '
               f'avg={float(r["AverageNs"])/1e3:9.2f} us  {float(r["Percentage"]):5.1f}%  {short}')
+
+
+def _short(name):
+    m = re.match(r"(?:void )?(?:\(anonymous namespace\)::)?([\w:<>, ]+?)\(", name)
+    short = (m.group(1) if m else name)[:70]
+    return name[:40] if short.startswith("Cijk") else short
+
+
+def _table(rows, total, n, per=1):
+    out = []
+    for name, (calls, ns) in sorted(rows.items(), key=lambda kv: -kv[1][1])[:n]:
+        out.append(f"{ns / 1e6 / per:9.3f} ms  calls={calls / per:7.1f}  avg={ns / calls / 1e3:9.2f} us  "
+                   f"{100.0 * ns / total if total else 0.0:5.1f}%  {_short(name)}")
+    return out
+
+
+def split(trace, steps, n=30):
+    """Kernels dispatched between the two marker spin kernels of bench.py (QVIT_STEP_MARKERS=1) are the timed steps'
+    kernels; everything before the first / after the second marker (library build checks, calibration, epilogue
+    tables, the event-timed second pass, parity/reference launches) is setup/parity."""
+    rows = sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Start_Timestamp"]))
+    marks = [i for i, r in enumerate(rows) if "spin_kernel" in r["Kernel_Name"]]
+    if len(marks) < 2:
+        raise SystemExit(f"{trace}: {len(marks)} marker spin kernels (run bench.py with QVIT_STEP_MARKERS=1)")
+    a, b = marks[0], marks[1]
+    step, other = {}, {}
+    for i, r in enumerate(rows):
+        if i in (a, b):
+            continue
+        d = step if a < i < b else other
+        ns = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        c = d.setdefault(r["Kernel_Name"], [0, 0])
+        c[0] += 1
+        c[1] += ns
+    span = int(rows[b]["Start_Timestamp"]) - int(rows[a]["End_Timestamp"])
+    st = sum(v[1] for v in step.values())
+    ot = sum(v[1] for v in other.values())
+    lines = [f"== timed steps: {steps} steps, {sum(v[0] for v in step.values())} dispatches "
+             f"({sum(v[0] for v in step.values()) / steps:.1f} per step), kernel time {st / 1e6 / steps:.3f} ms per step, "
+             f"marker-to-marker span {span / 1e6 / steps:.3f} ms per step (rows: per step)"]
+    lines += _table(step, st, n, per=steps)
+    lines += ["", f"== setup / calibration / event-timed pass / parity (NOT the step): "
+                  f"{sum(v[0] for v in other.values())} dispatches, {ot / 1e6:.3f} ms total (rows: whole run)"]
+    lines += _table(other, ot, n)
+    print("\n".join(lines))
 
 
 def pmc_values(d, counter):
@@ -104,5 +153,7 @@ if __name__ == "__main__":
     if sys.argv[1] == "--pmc":
         rnd = sys.argv[sys.argv.index("--round") + 1] if "--round" in sys.argv else "r01"
         pmc(sys.argv[2], sys.argv[3], rnd)
+    elif sys.argv[1] == "--split":
+        split(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]) if len(sys.argv) > 4 else 30)
     else:
         top(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 25)
