@@ -70,9 +70,14 @@ _SIGNATURES = {
     "qvit_gemm_a32_fits": [_i64, _i32, _i64, _i64, _i32],
     "qvit_gemm_a32": [_c_p, _i64, _i64, _c_p, _i32, _i64, _i64, _c_p, _c_p, _c_p, _i32, _c_p, _i64, _i32, _c_p, _c_p,
                       _c_p, _i32, _c_p, _c_p],
+    "qvit_gemm_sk": [_c_p, _i64, _i64, _i64, _c_p, _i32, _i64, _i64, _c_p, _c_p, _c_p, _i32, _c_p, _i64, _c_p, _i64,
+                     _c_p],
     "qvit_gemm_wonly": [_c_p, _i64, _i64, _i64, _c_p, _i32, _i64, _i64, _c_p, _c_p, _c_p, _i64, _c_p, _i64, _c_p],
     "qvit_conv_wonly": [_c_p, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _c_p, _i32,
                         _i64, _i64, _i64, _c_p, _c_p, _c_p, _c_p, _i64, _c_p],
+    "qvit_conv_wonly_bn_act": [_c_p, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _c_p,
+                               _i32, _i64, _i64, _i64, _c_p, _c_p, _c_p, _c_p, _i32, _c_p, _c_p],
+    "qvit_conv_wonly_narrow": [_i32],
     "qvit_epi_table_build": [_i32, _i32, _c_p, _c_p, _c_p, _i32, _f32, _f32, _i64, _c_p, _c_p],
     "qvit_gemm_resid_ln": [_c_p, _i64, _i64, _i64, _c_p, _i32, _i64, _i64, _c_p, _c_p, _c_p, _c_p, _i64, _c_p, _c_p,
                            _f32, _i32, _c_p, _c_p, _c_p, _i32, _c_p, _c_p, _i64, _i64, _c_p, _c_p],
@@ -96,8 +101,12 @@ _SIGNATURES = {
     "qvit_attention_split": [_c_p, _c_p, _i64, _i64, _i64, _i64, _f32, _f32, _i32, _c_p, _i64, _i32, _c_p, _c_p,
                              _c_p, _i32, _c_p, _c_p],
 }
+# name -> argtypes of the entry points returning int64_t
+INT64_FUNCS = {
+    "qvit_gemm_sk_workspace_bytes": [_i64, _i64, _i64, _i64, _i32],
+}
 STRING_FUNCS = {"qvit_strerror": [_i32], "qvit_version": []}
-EXPORTED_SYMBOLS = sorted(list(_SIGNATURES) + list(STRING_FUNCS))
+EXPORTED_SYMBOLS = sorted(list(_SIGNATURES) + list(INT64_FUNCS) + list(STRING_FUNCS))
 
 _lock = threading.Lock()
 _lib: Optional[ctypes.CDLL] = None
@@ -124,6 +133,12 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
             fn = getattr(lib, name)
             fn.argtypes = args
             fn.restype = ctypes.c_int
+        for name, args in INT64_FUNCS.items():
+            if path != LIB_PATH and not hasattr(lib, name):
+                continue
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = ctypes.c_int64
         for name, args in STRING_FUNCS.items():
             fn = getattr(lib, name)
             fn.argtypes = args
@@ -289,6 +304,38 @@ def gemm(A: torch.Tensor, M: int, K: int, packed: torch.Tensor, wfmt: int, N: in
     return C
 
 
+_SK_WS: dict = {}
+
+
+def sk_workspace(device: torch.device, M: int, K: int, lda: int, npad: int, wfmt: int) -> Optional[torch.Tensor]:
+    """The stream-K workspace of qvit_gemm_sk for this device and stream: arrival counters (zero between launches:
+    every launch leaves them zero) + the split tiles' int32 partials. Allocated zeroed once and grown on demand;
+    one per stream, so launches on different streams never share it. None when the library lacks the entry."""
+    lib = load()
+    if not hasattr(lib, "qvit_gemm_sk_workspace_bytes"):
+        return None
+    need = int(lib.qvit_gemm_sk_workspace_bytes(M, K, lda, npad, wfmt))
+    if need <= 0:
+        return None
+    key = (device, torch.cuda.current_stream(device).cuda_stream)
+    ws = _SK_WS.get(key)
+    if ws is None or ws.numel() < need:
+        ws = torch.zeros(need, dtype=torch.uint8, device=device)
+        _SK_WS[key] = ws
+    return ws
+
+
+def gemm_sk(A: torch.Tensor, M: int, K: int, packed: torch.Tensor, wfmt: int, N: int, npad: int, d_act, d_wt,
+            bias_pad: Optional[torch.Tensor], epilogue: int, C: torch.Tensor, workspace: torch.Tensor) -> torch.Tensor:
+    """qvit_gemm for the fp32 epilogues with the stream-K tail (the XCD's last partial round of tiles split along K
+    over every workgroup; bit-identical to qvit_gemm)."""
+    _require_gpu(A, "codes")
+    _check(load().qvit_gemm_sk(_ptr(A), M, K, A.stride(0), _ptr(packed), wfmt, N, npad, _ptr(d_act), _ptr(d_wt),
+                               _ptr(bias_pad), epilogue, _ptr(C), C.stride(0), _ptr(workspace), workspace.numel(),
+                               _stream(A.device)), "qvit_gemm_sk")
+    return C
+
+
 def t32_rows(M: int) -> int:
     """Rows a QVIT_ACT_T32 code buffer holds for M rows (whole 64-row wave tiles of qvit_gemm_a32)."""
     return (M + 63) // 64 * 64
@@ -380,12 +427,53 @@ def conv_wonly(x: torch.Tensor, kernel_size, stride, padding, dilation, packed: 
     OW = (W + 2 * pw - dw * (kw - 1) - 1) // sw + 1
     y = torch.empty((B, N, OH, OW), dtype=torch.float32, device=x.device)
     M = B * OH * OW
-    small = (npad // 256) * ((M + 63) // 64) < 128
+    small = (npad // 256) * ((M + 63) // 64) < 128 and not narrow_conv_fits(wfmt, N, C * kh * kw)  # (no split)
     ws = wonly_workspace(x.device, M, npad) if small else None
     _check(load().qvit_conv_wonly(_ptr(x), B, C, H, W, kh, kw, sh, sw, ph, pw, dh, dw, _ptr(packed), wfmt, N, npad,
                                   kpad, _ptr(d_wt), _ptr(bias_pad), _ptr(y), _ptr(ws),
                                   0 if ws is None else ws.numel() * 4, _stream(x.device)), "qvit_conv_wonly")
     return y
+
+
+def conv_wonly_bn_act(x: torch.Tensor, kernel_size, stride, padding, dilation, packed: torch.Tensor, wfmt: int,
+                      N: int, npad: int, kpad: int, d_wt: torch.Tensor, bias_pad: Optional[torch.Tensor],
+                      bn_alpha: torch.Tensor, bn_shift: torch.Tensor, a_levels: int) -> Optional[torch.Tensor]:
+    """conv_wonly -> BatchNorm2d(eval) as y alpha + shift (ultra_bn_fold) -> activation_quantize_fn values
+    round(clamp(., 0, 1) levels) / levels, in one launch (qvit_conv_wonly_bn_act, the narrow schedule). None when
+    the layer is outside that schedule (more than 64 channels, codes wider than int8, a weight panel past 24 KiB):
+    the caller runs the modules one by one."""
+    _require_gpu(x, "activations")
+    (kh, kw), (sh, sw), (ph, pw), (dh, dw) = kernel_size, stride, padding, dilation
+    if not narrow_conv_fits(wfmt, N, x.shape[1] * kh * kw):
+        return None
+    if x.dtype != torch.float32 or not x.is_contiguous():
+        x = x.float().contiguous()
+    B, C, H, W = x.shape
+    OH = (H + 2 * ph - dh * (kh - 1) - 1) // sh + 1
+    OW = (W + 2 * pw - dw * (kw - 1) - 1) // sw + 1
+    y = torch.empty((B, N, OH, OW), dtype=torch.float32, device=x.device)
+    _check(load().qvit_conv_wonly_bn_act(_ptr(x), B, C, H, W, kh, kw, sh, sw, ph, pw, dh, dw, _ptr(packed), wfmt, N,
+                                       npad, kpad, _ptr(d_wt), _ptr(bias_pad), _ptr(bn_alpha), _ptr(bn_shift),
+                                       a_levels, _ptr(y), _stream(x.device)), "qvit_conv_wonly_bn_act")
+    return y
+
+
+NARROW_W_MAX = 24 * 1024   # gemm_wonly.hip NW_WMAX: the narrow schedule's LDS weight panel
+
+
+def narrow_conv_fits(wfmt: int, N: int, kreal: int) -> bool:
+    """Whether qvit_conv_wonly runs the narrow schedule (gemm_wonly.hip narrow_geo): N <= 64 channels, int4 / int8
+    codes, the K stages up to C kh kw of 16 ceil(N / 16) rows within NARROW_W_MAX, the schedule enabled."""
+    if N > 64 or wfmt not in (W4, W8) or not conv_wonly_narrow(-1):
+        return False
+    nke = (kreal + 63) // 64
+    return nke * 16 * ((N + 15) // 16) * (32 if wfmt == W4 else 64) <= NARROW_W_MAX
+
+
+def conv_wonly_narrow(enable: int = -1) -> bool:
+    """The narrow convolution schedule of qvit_conv_wonly (N <= 64) on (1) / off (0) for this process; -1 queries.
+    Returns the previous setting (tests compare the two schedules)."""
+    return bool(load().qvit_conv_wonly_narrow(int(enable)))
 
 
 def resid_ln_counters(device: torch.device, rows: int, npad: int) -> torch.Tensor:

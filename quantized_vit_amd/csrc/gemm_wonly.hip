@@ -322,6 +322,255 @@ __global__ __launch_bounds__(256) void wonly_reduce_kernel(const float* __restri
     if (n + j < N) yr[j] = fmaf(alpha, a[j], bias ? bias[n + j] : 0.f);
 }
 
+// ---- narrow convolution (N <= 64 output channels, UltraNet's Conv2d_Q layers) -----------------------------------
+// The wide kernel's 256-row weight tile is 75-94 % padding for 16-64 output channels. Here all N features (NT
+// MFMA tiles of 16) of all K stages sit in LDS for the workgroup's lifetime (loaded once, re-ordered from the
+// packed image so that LDS row f = feature f), and the workgroup walks 64-pixel tiles: wave w computes pixels
+// 16 w .. 16 w + 15 of the tile against the NT feature tiles. The patch gather is transposed too: lane = pixel,
+// wave = 16-tap quarter of the 64-deep stage, so the tap (c, ky, kx) and its input offset are wave-uniform (scalar)
+// and every tap load reads 64 consecutive output pixels' inputs; quarters and stages past C kh kw are skipped.
+// MFMAs, their operands and their order per accumulator (stage, chunk c, bf16 plane p) are the wide kernel's, so
+// the results are bit-identical to it (tests/test_gpu_ultra_modules.py::test_conv_wonly_narrow_equals_wide).
+// EPI 0: y = (d_w / s) acc + bias; EPI 1 (qvit_conv_wonly_bn_act, Conv2d_Q -> BatchNorm2d(eval) ->
+// activation_quantize_fn): z = y alpha_n + shift_n (fp32 multiply, then add: the fold ultra_bn_fold computes)
+// -> round(clamp(z, 0, 1) levels) / levels.
+constexpr int NW_BM = 64;                              // pixels per tile
+constexpr int NW_WMAX = 24 * 1024;                     // weight panel bytes (two workgroups per CU)
+constexpr int NW_LDS = 2 * WO_XBYTES + NW_WMAX + 3 * 64 * 4;
+static_assert(2 * NW_LDS <= 163840, "two workgroups per CU");
+
+bool g_wonly_narrow = true;
+
+template <int WFMT, int NT, int EPI>
+__global__ __launch_bounds__(256, 2) void conv_wonly_narrow_kernel(
+    const float* __restrict__ X, int M, int nke, const int8_t* __restrict__ Wp, int N,
+    const float* __restrict__ d_wt, const float* __restrict__ bias, const float* __restrict__ bn_a,
+    const float* __restrict__ bn_s, float levels, float* __restrict__ Y, const WoConv cg) {
+  using G = WoGeo<WFMT>;
+  constexpr int NF = 16 * NT;                          // feature rows held
+  __shared__ __attribute__((aligned(16))) int8_t nw_smem[NW_LDS];
+  int8_t* xs_l = nw_smem;                              // 2 x-stages (3 bf16 planes each)
+  int8_t* w_l = nw_smem + 2 * WO_XBYTES;               // [stage][NF rows][WROW]
+  float* bias_l = reinterpret_cast<float*>(w_l + nke * NF * G::WROW);
+  float* bna_l = bias_l + NF;
+  float* bns_l = bna_l + NF;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // weight panel: LDS row f of stage st = packed row rho(f) (perm_row's inverse inside the first 64-row group),
+  // chunks re-swizzled from rho's position to f's
+  {
+    constexpr int CH = G::WROW / 4;                    // 8 (W4) / 16 (W8) bytes per chunk
+    const int units = nke * NF * 4;
+    for (int u = tid; u < units; u += 256) {
+      const int c = u & 3, f = (u >> 2) % NF, st = (u >> 2) / NF;
+      const int rho = 16 * ((f >> 2) & 3) + 4 * (f >> 4) + (f & 3);
+      const int sw_src = WFMT == QVIT_W4 ? ((rho >> 3) & 1) << 1 : ((rho >> 2) & 1) << 1;
+      const int sw_dst = WFMT == QVIT_W4 ? ((f >> 3) & 1) << 1 : ((f >> 2) & 1) << 1;
+      const int8_t* src = Wp + (int64_t)st * G::WBYTES + rho * G::WROW + CH * (c ^ sw_src);
+      int8_t* dst = w_l + (st * NF + f) * G::WROW + CH * (c ^ sw_dst);
+      if (CH == 8) *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(src);
+      else *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+    }
+    for (int f = tid; f < NF; f += 256) {
+      bias_l[f] = (bias && f < N) ? bias[f] : 0.f;
+      if (EPI == 1) {
+        bna_l[f] = f < N ? bn_a[f] : 0.f;
+        bns_l[f] = f < N ? bn_s[f] : 0.f;
+      }
+    }
+  }
+
+  const int ntiles = (M + NW_BM - 1) / NW_BM;
+  const int my = ntiles > (int)blockIdx.x ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int units = my * nke;
+  const int khw = cg.kh * cg.kw;
+
+  // the load side: this lane's pixel of the tile being loaded (lane = pixel, wave = quarter)
+  int64_t lbase = 0;
+  int iy0 = 0, ix0 = 0;
+  bool mval = false;
+  auto pixel = [&](int tile) __attribute__((always_inline)) {
+    const int m = tile * NW_BM + lane;
+    mval = m < M;
+    const int mm = mval ? m : M - 1;
+    const int b = mm / cg.L, p = mm - b * cg.L, oy = p / cg.OW;
+    iy0 = oy * cg.sh - cg.ph;
+    ix0 = (p - oy * cg.OW) * cg.sw - cg.pw;
+    lbase = (int64_t)b * cg.C * cg.H * cg.W + (int64_t)iy0 * cg.W + ix0;
+  };
+  float xv[16];
+  auto load = [&](int u) __attribute__((always_inline)) {
+    const int i = u / nke, st = u - i * nke;
+    if (st == 0) pixel((int)blockIdx.x + i * (int)gridDim.x);
+    const int k0 = st * WO_BK + 16 * wave;             // wave-uniform
+    if (k0 >= cg.kreal) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) xv[e] = 0.f;
+      return;
+    }
+    int c = k0 / khw, r = k0 - c * khw, ky = r / cg.kw, kx = r - ky * cg.kw;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      float v = 0.f;
+      if (k0 + e < cg.kreal) {
+        const int dy = ky * cg.dh, dx = kx * cg.dw;
+        const bool ok = mval && (unsigned)(iy0 + dy) < (unsigned)cg.H && (unsigned)(ix0 + dx) < (unsigned)cg.W;
+        const int64_t idx = ok ? lbase + ((int64_t)c * cg.H + dy) * cg.W + dx : 0;
+        v = X[idx];
+        v = ok ? v : 0.f;
+      }
+      xv[e] = v;
+      if (++kx == cg.kw) {
+        kx = 0;
+        if (++ky == cg.kh) {
+          ky = 0;
+          ++c;
+        }
+      }
+    }
+  };
+  auto store = [&](int b) __attribute__((always_inline)) {
+    uint32_t p1[8], p2[8], p3[8];
+#pragma unroll
+    for (int e = 0; e < 16; e += 2) {
+      const float a = xv[e], c = xv[e + 1];
+      const float a1 = trunc_bf16(a), c1 = trunc_bf16(c);
+      const float ar = a - a1, cr = c - c1;
+      const float a2 = trunc_bf16(ar), c2 = trunc_bf16(cr);
+      const float a3 = ar - a2, c3 = cr - c2;
+      p1[e >> 1] = hi16(a1, c1);
+      p2[e >> 1] = hi16(a2, c2);
+      p3[e >> 1] = hi16(a3, c3);
+    }
+    int8_t* d = xs_l + b * WO_XBYTES + lane * WO_PITCH + 32 * wave;
+    *reinterpret_cast<uint4*>(d) = make_uint4(p1[0], p1[1], p1[2], p1[3]);
+    *reinterpret_cast<uint4*>(d + 16) = make_uint4(p1[4], p1[5], p1[6], p1[7]);
+    *reinterpret_cast<uint4*>(d + WO_PLANE) = make_uint4(p2[0], p2[1], p2[2], p2[3]);
+    *reinterpret_cast<uint4*>(d + WO_PLANE + 16) = make_uint4(p2[4], p2[5], p2[6], p2[7]);
+    *reinterpret_cast<uint4*>(d + 2 * WO_PLANE) = make_uint4(p3[0], p3[1], p3[2], p3[3]);
+    *reinterpret_cast<uint4*>(d + 2 * WO_PLANE + 16) = make_uint4(p3[4], p3[5], p3[6], p3[7]);
+  };
+
+  const int woff = (WFMT == QVIT_W4) ? fr * G::WROW + ((fq ^ (((fr >> 3) & 1) << 1)) << 3)
+                                     : fr * G::WROW + ((fq ^ (((fr >> 2) & 1) << 1)) << 4);
+  const int xoff = (16 * wave + fr) * WO_PITCH + 32 * fq;
+  const float alpha = (*d_wt) * (WFMT == QVIT_W4 ? 0.0625f : 1.f);
+  f4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+
+  if (units > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();  // (also publishes the weight panel)
+  for (int u = 0; u < units; ++u) {
+    const int i = u / nke, st = u - i * nke;
+    if (u + 1 < units) load(u + 1);
+    const int8_t* base = xs_l + (u & 1) * WO_XBYTES;
+    bf8 wb[NT][2];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int8_t* wp = w_l + (st * NF + 16 * t) * G::WROW + woff;
+      v4i wf;
+      if (WFMT == QVIT_W4) {
+        const uint2 p = *reinterpret_cast<const uint2*>(wp);
+        wf = v4i{(int)nib16_lo(p.x), (int)nib16_hi(p.x), (int)nib16_lo(p.y), (int)nib16_hi(p.y)};
+      } else {
+        wf = *reinterpret_cast<const v4i*>(wp);
+      }
+      uint32_t h[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bytes_bf16((uint32_t)wf[e], h[2 * e], h[2 * e + 1], 1.f);
+      wb[t][0] = __builtin_bit_cast(bf8, make_uint4(h[0], h[1], h[2], h[3]));
+      wb[t][1] = __builtin_bit_cast(bf8, make_uint4(h[4], h[5], h[6], h[7]));
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      bf8 xsv[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) xsv[p] = *reinterpret_cast<const bf8*>(base + xoff + 16 * c + p * WO_PLANE);
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[t][c], xsv[p], acc[t], 0, 0, 0);
+    }
+    if (st == nke - 1) {
+      // epilogue of tile i: lane (fr, fq) holds features 16 t + 4 fq + j of pixel 16 wave + fr
+      const int m = ((int)blockIdx.x + i * (int)gridDim.x) * NW_BM + 16 * wave + fr;
+      if (m < M) {
+        const int b = m / cg.L;
+        float* yp = Y + ((int64_t)b * N * cg.L + (m - b * cg.L));
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int n = 16 * t + 4 * fq + j;
+            float y = fmaf(alpha, acc[t][j], bias_l[n]);
+            if (EPI == 1) {
+              const float z = __fadd_rn(__fmul_rn(y, bna_l[n]), bns_l[n]);
+              y = rintf(fminf(fmaxf(z, 0.f), 1.f) * levels) / levels;
+            }
+            if (n < N) yp[(int64_t)n * cg.L] = y;
+          }
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (u + 1 < units) store((u + 1) & 1);  // the other buffer: its last reader finished a barrier ago
+    __syncthreads();
+  }
+}
+
+// the narrow schedule's stage count, LDS bytes and feature tiles, or 0 when it does not apply
+struct NarrowGeo {
+  int nke, nt, lds;
+};
+NarrowGeo narrow_geo(int wfmt, int64_t N, int64_t npad, int64_t kreal, int64_t K) {
+  if (!g_wonly_narrow || (wfmt != QVIT_W4 && wfmt != QVIT_W8) || N > 64 || npad < 64) return {0, 0, 0};
+  const int nke = (int)((kreal + WO_BK - 1) / WO_BK);
+  const int nt = (int)((N + 15) / 16);
+  const int wrow = wfmt == QVIT_W4 ? 32 : 64;
+  const int64_t wbytes = (int64_t)nke * 16 * nt * wrow;
+  if (nke < 1 || nke > K / WO_BK || wbytes > NW_WMAX) return {0, 0, 0};
+  return {nke, nt, (int)(2 * WO_XBYTES + wbytes + 3 * 16 * nt * 4)};  // (lds: the bytes used of NW_LDS)
+}
+
+template <int EPI>
+int narrow_launch(const NarrowGeo& g, const float* X, int64_t M, const int8_t* w, int wfmt, int64_t N,
+                  const float* d_wt, const float* bias, const float* bn_a, const float* bn_s, float levels, float* Y,
+                  const WoConv& cg, hipStream_t stream) {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess || n <= 0)
+      n = 256;
+    return n;
+  }();
+  const int64_t ntiles = (M + NW_BM - 1) / NW_BM;
+  const unsigned grid = (unsigned)std::min<int64_t>(ntiles, 2 * (int64_t)cus);
+#define QVIT_NW(F, T)                                                                                            \
+  hipLaunchKernelGGL((conv_wonly_narrow_kernel<F, T, EPI>), dim3(grid), dim3(256), 0, stream, X, (int)M, g.nke, w, \
+                     (int)N, d_wt, bias, bn_a, bn_s, levels, Y, cg)
+#define QVIT_NW_T(F)      \
+  switch (g.nt) {         \
+    case 1: QVIT_NW(F, 1); break; \
+    case 2: QVIT_NW(F, 2); break; \
+    case 3: QVIT_NW(F, 3); break; \
+    default: QVIT_NW(F, 4); break; \
+  }
+  if (wfmt == QVIT_W4) {
+    QVIT_NW_T(QVIT_W4)
+  } else {
+    QVIT_NW_T(QVIT_W8)
+  }
+#undef QVIT_NW_T
+#undef QVIT_NW
+  return qvit_hip_status(hipGetLastError());
+}
+
 // shared launch of the GEMM (CONV = false) and the implicit-GEMM convolution (CONV = true); arguments checked
 template <bool CONV>
 int wonly_launch(const float* X, int64_t M, int64_t K, int64_t ldx, const void* Wp, int wfmt, int64_t N, int64_t npad,
@@ -329,6 +578,12 @@ int wonly_launch(const float* X, int64_t M, int64_t K, int64_t ldx, const void* 
                  const WoConv& cg, hipStream_t stream) {
   const int64_t ntiles = (npad / WO_BN) * ((M + WO_BM - 1) / WO_BM);
   if (ntiles > INT32_MAX / 2) return QVIT_EINVAL;
+  if (CONV) {  // few output channels: the narrow schedule
+    const NarrowGeo g = narrow_geo(wfmt, N, npad, cg.kreal, K);
+    if (g.nke > 0)
+      return narrow_launch<0>(g, X, M, reinterpret_cast<const int8_t*>(Wp), wfmt, N, d_wt, bias, nullptr, nullptr,
+                              0.f, Y, cg, stream);
+  }
   // fewer tiles than half the CUs: split the K stages so that about 256 workgroups run (when the workspace
   // holds the partials)
   const int64_t nk = K / WO_BK;
@@ -378,10 +633,12 @@ extern "C" int qvit_gemm_wonly(const float* X, int64_t M, int64_t K, int64_t ldx
                              WoConv{}, stream);
 }
 
-extern "C" int qvit_conv_wonly(const float* X, int64_t B, int64_t C, int64_t H, int64_t W, int kh, int kw, int sh,
-                               int sw, int ph, int pw, int dh, int dw, const void* Wp, int wfmt, int64_t N,
-                               int64_t npad, int64_t K, const float* d_wt, const float* bias, float* Y,
-                               float* workspace, int64_t workspace_bytes, hipStream_t stream) {
+namespace {
+
+// the argument checks of the convolution entries; fills cg and M
+int conv_args(const float* X, int64_t B, int64_t C, int64_t H, int64_t W, int kh, int kw, int sh, int sw, int ph,
+              int pw, int dh, int dw, const void* Wp, int wfmt, int64_t N, int64_t npad, int64_t K, const float* d_wt,
+              const float* bias, float* Y, WoConv& cg, int64_t& M) {
   if (!X || !Wp || !Y || !d_wt) return QVIT_ENULL;
   if (wfmt != QVIT_W4 && wfmt != QVIT_W8 && wfmt != QVIT_W16 && wfmt != QVIT_W24) return QVIT_EINVAL;
   if (B < 0 || C <= 0 || H <= 0 || W <= 0 || kh <= 0 || kw <= 0 || sh <= 0 || sw <= 0 || ph < 0 || pw < 0 ||
@@ -395,10 +652,47 @@ extern "C" int qvit_conv_wonly(const float* X, int64_t B, int64_t C, int64_t H, 
   if (K <= 0 || K % QVIT_TILE_K || K < kreal || K > (1 << 24) || N <= 0 || npad < N || npad % WO_BN ||
       npad > INT32_MAX / 2)
     return QVIT_EINVAL;
-  const int64_t M = B * OH * OW;
+  M = B * OH * OW;
   if (M > INT32_MAX / 2 || OH * OW > INT32_MAX / 2) return QVIT_EINVAL;
   if ((((uintptr_t)Wp) & 15) || (bias && (((uintptr_t)bias) & 15))) return QVIT_EALIGN;
+  cg = WoConv{(int)C, (int)H, (int)W, kh, kw, sh, sw, ph, pw, dh, dw, (int)OW, (int)(OH * OW), (int)kreal};
+  return QVIT_OK;
+}
+
+}  // namespace
+
+extern "C" int qvit_conv_wonly(const float* X, int64_t B, int64_t C, int64_t H, int64_t W, int kh, int kw, int sh,
+                               int sw, int ph, int pw, int dh, int dw, const void* Wp, int wfmt, int64_t N,
+                               int64_t npad, int64_t K, const float* d_wt, const float* bias, float* Y,
+                               float* workspace, int64_t workspace_bytes, hipStream_t stream) {
+  WoConv cg{};
+  int64_t M = 0;
+  const int st = conv_args(X, B, C, H, W, kh, kw, sh, sw, ph, pw, dh, dw, Wp, wfmt, N, npad, K, d_wt, bias, Y, cg, M);
+  if (st != QVIT_OK) return st;
   if (M == 0) return QVIT_OK;
-  const WoConv cg{(int)C, (int)H, (int)W, kh, kw, sh, sw, ph, pw, dh, dw, (int)OW, (int)(OH * OW), (int)kreal};
   return wonly_launch<true>(X, M, K, K, Wp, wfmt, N, npad, d_wt, bias, Y, N, workspace, workspace_bytes, cg, stream);
+}
+
+extern "C" int qvit_conv_wonly_bn_act(const float* X, int64_t B, int64_t C, int64_t H, int64_t W, int kh, int kw,
+                                      int sh, int sw, int ph, int pw, int dh, int dw, const void* Wp, int wfmt,
+                                      int64_t N, int64_t npad, int64_t K, const float* d_wt, const float* bias,
+                                      const float* bn_alpha, const float* bn_shift, int a_levels, float* Y,
+                                      hipStream_t stream) {
+  WoConv cg{};
+  int64_t M = 0;
+  const int st = conv_args(X, B, C, H, W, kh, kw, sh, sw, ph, pw, dh, dw, Wp, wfmt, N, npad, K, d_wt, bias, Y, cg, M);
+  if (st != QVIT_OK) return st;
+  if (!bn_alpha || !bn_shift) return QVIT_ENULL;
+  if (a_levels < 1 || a_levels > 127) return QVIT_EINVAL;
+  const NarrowGeo g = narrow_geo(wfmt, N, npad, cg.kreal, K);
+  if (g.nke == 0) return QVIT_EINVAL;  // (N > 64, W16 / W24, or a weight panel past NW_WMAX: unfused modules)
+  if (M == 0) return QVIT_OK;
+  return narrow_launch<1>(g, X, M, reinterpret_cast<const int8_t*>(Wp), wfmt, N, d_wt, bias, bn_alpha, bn_shift,
+                          (float)a_levels, Y, cg, stream);
+}
+
+extern "C" int qvit_conv_wonly_narrow(int enable) {
+  const int prev = g_wonly_narrow ? 1 : 0;
+  if (enable >= 0) g_wonly_narrow = enable != 0;
+  return prev;
 }

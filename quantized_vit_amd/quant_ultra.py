@@ -5,7 +5,9 @@ UltraNet): same factory / class names and forward semantics, computed on the ROC
   weight_quantize_fn(w_bit)  :30-56   tanh -> / max|tanh| -> (w_bit-1)-bit uniform quantizer (HIP codes)
   activation_quantize_fn     :59-73   clamp(x, 0, 1) -> a_bit uniform quantizer (HIP)
   conv2d_Q_fn(w_bit)         :76-91   Conv2d_Q: conv with quantized weights -- qvit_conv_wonly (implicit GEMM of the
-                                      fp32 input against the int weight codes, d_w = 1/(2^(w_bit-1)-1))
+                                      fp32 input against the int weight codes, d_w = 1/(2^(w_bit-1)-1); <= 64
+                                      output channels: the narrow schedule); forward_bn_act fuses a following
+                                      eval BatchNorm2d + activation_quantize_fn (qvit_conv_wonly_bn_act)
   linear_Q_fn(w_bit)         :210-222 Linear_Q -- qvit_gemm_wonly on the same codes
   batchNorm2d_Q_fn / batchNorm1d_Q_fn  :94-207 (not used by UltraNetQua; kept for API parity)
 
@@ -150,6 +152,7 @@ def conv2d_Q_fn(w_bit):
             self.w_bit = w_bit
             self.quantize_fn = weight_quantize_fn(w_bit=w_bit)
             self._codes = _PackedCodes()
+            self._bn_fold = None   # (key, alpha, shift) of the BatchNorm2d forward_bn_act last fused
 
         def prepare(self):
             """Packs the weight codes now (cached per weight version; see QuantizeMixin.prepare)."""
@@ -158,9 +161,11 @@ def conv2d_Q_fn(w_bit):
             return self
 
         def invalidate(self):
-            """Drops the packed codes: needed only after editing the weight or bias through `.data` (which bypasses the
-            version counter the cache keys on; QuantizeMixin.invalidate alike)."""
+            """Drops the packed codes (and the fused BatchNorm fold): needed only after editing the weight, bias or BN
+            statistics through `.data` (which bypasses the version counter the caches key on; QuantizeMixin.invalidate
+            alike)."""
             self._codes.key = None
+            self._bn_fold = None
             return self
 
         def forward(self, input, order=None):
@@ -173,6 +178,30 @@ def conv2d_Q_fn(w_bit):
                                        c.packed, c.wfmt, c.n, c.npad, c.kpad, c.d_wt, c.bias_pad)
             weight_q = self.quantize_fn(self.weight)
             return F.conv2d(input, weight_q, self.bias, self.stride, self.padding, self.dilation, self.groups)
+
+        def forward_bn_act(self, input, bn, act):
+            """act(bn(self(input))) in one launch when `bn` is a BatchNorm2d in eval mode on running statistics and
+            `act` an activation_quantize_fn with 1 <= a_bit <= 7 (UltraNet's conv -> BN -> quantizer blocks,
+            mymodel.py:71-124): qvit_conv_wonly_bn_act, BN as y alpha + shift (alpha = gamma / sqrt(var + eps),
+            shift = beta - mean alpha: the fused network's fold, ultra_bn_fold) and the quantizer's values
+            round(clamp(., 0, 1) n) / n. Returns None when the three modules do not fit that launch (the caller then
+            runs them one by one)."""
+            if not (_codes_path(self.w_bit) and self.groups == 1 and self.padding_mode == "zeros"
+                    and not isinstance(self.padding, str) and input.dim() == 4 and input.is_cuda
+                    and isinstance(bn, nn.BatchNorm2d) and not bn.training and bn.track_running_stats
+                    and bn.running_mean is not None and bn.running_var is not None
+                    and bn.num_features == self.out_channels
+                    and isinstance(act, activation_quantize_fn) and 1 <= act.a_bit <= 7
+                    and not _needs_grad(self, input) and not _needs_grad(bn, input)):
+                return None
+            c = self._codes.get(self.weight, self.bias, self.w_bit)
+            key = tuple((t.data_ptr(), t._version) for t in (bn.weight, bn.bias, bn.running_mean, bn.running_var)
+                        if t is not None) + (bn.eps, input.device)
+            if self._bn_fold is None or self._bn_fold[0] != key:
+                self._bn_fold = (key, *_lib.ultra_bn_fold(bn, input.device))
+            return _lib.conv_wonly_bn_act(input.detach(), self.kernel_size, self.stride, self.padding, self.dilation,
+                                          c.packed, c.wfmt, c.n, c.npad, c.kpad, c.d_wt, c.bias_pad, self._bn_fold[1],
+                                          self._bn_fold[2], 2 ** act.a_bit - 1)
 
     return Conv2d_Q
 

@@ -215,13 +215,23 @@ class UltraNetQua(nn.Module):
     def forward_modules(self, x):
         """mymodel.py:134-144 module by module: Conv2d_Q on qvit_conv_wonly, activation_quantize_fn on the HIP
         quantizer; BatchNorm2d and MaxPool2d on ATen's own kernels (the MIOpen batch-norm route off, so no
-        library kernel is on the path). Any image size, training mode included; under autograd (grad mode on and a
+        library kernel is on the path). In eval mode each Conv2d_Q -> BatchNorm2d -> activation_quantize_fn triple
+        runs as one launch (Conv2d_Q.forward_bn_act: the BN applied as the fused network folds it); the
+        Sequential's own forward hooks are not called on this walk. Any image size, training mode included; under autograd (grad mode on and a
         parameter or the input requiring grad) the Conv2d_Q layers take the reference's F.conv2d on the fake-quant
         weight instead, so gradients flow (the packed-codes kernels record no history)."""
         img_size = x.shape[-2:]
         yolo_out = []
         with _aten_batch_norm():
-            x = self.layers(x)
+            mods, i = list(self.layers), 0
+            while i < len(mods):
+                m = mods[i]
+                if hasattr(m, "forward_bn_act") and i + 2 < len(mods):
+                    y = m.forward_bn_act(x, mods[i + 1], mods[i + 2])   # conv -> BN -> quantizer in one launch
+                    if y is not None:
+                        x, i = y, i + 3
+                        continue
+                x, i = m(x), i + 1
         x = self.yololayer(x, img_size)
         yolo_out.append(x)
         if self.training:

@@ -57,6 +57,8 @@ GEOMETRIES = [
     (2, 3, 64, 64, 300, 16, 16, (16, 16), (0, 0), (1, 1), _lib.W4),  # patch embedding, N > 256
     (1, 5, 7, 7, 9, 3, 3, (1, 1), (3, 3), (1, 1), _lib.W8),         # padding > kernel reach, split-K path
     (4, 64, 52, 52, 64, 3, 3, (1, 1), (1, 1), (1, 1), _lib.W4),     # UltraNet block 3 shape, no split
+    (1, 5, 7, 7, 80, 3, 3, (1, 1), (2, 2), (1, 1), _lib.W8),        # N > 64: the wide schedule's split-K path
+    (2, 64, 20, 18, 64, 3, 3, (1, 1), (1, 1), (1, 1), _lib.W8),     # int8 panel past 24 KiB: the wide schedule
 ]
 
 
@@ -75,6 +77,86 @@ def test_conv_wonly_geometries(dev, geo):
                         bias_pad)
     w = (codes.double() * d.double()).view(N, C, kh, kw)
     _assert_conv_close(y, x, w, bias, stride, padding, dilation)
+
+
+NARROW = [g for g in GEOMETRIES if g[4] <= 64] + [
+    (3, 40, 19, 17, 1, 3, 3, (1, 1), (1, 1), (1, 1), _lib.W4),      # one output channel, 6 stages
+    (2, 7, 25, 25, 48, 5, 5, (2, 1), (2, 2), (1, 1), _lib.W4),      # 3 feature tiles, ragged last stage
+]
+
+
+@pytest.mark.parametrize("geo", NARROW, ids=lambda g: "x".join(map(str, g[:7])) + f"w{g[10]}")
+def test_conv_wonly_narrow_equals_wide(dev, geo):
+    """The narrow schedule (N <= 64: LDS-resident weights, lane-per-pixel gather) gives the wide schedule's values
+    bit for bit: the same MFMAs on the same operands in the same order per accumulator."""
+    B, C, H, W, N, kh, kw, stride, padding, dilation, wfmt = geo
+    g = torch.Generator().manual_seed(B * 7 + C * 3 + N)
+    lvl = 7 if wfmt == _lib.W4 else 127
+    codes = torch.randint(-lvl, lvl + 1, (N, C * kh * kw), generator=g)
+    x = torch.randn(B, C, H, W, generator=g).to(dev)
+    bias = torch.randn(N, generator=g).to(dev)
+    d = torch.tensor([0.0213], device=dev)
+    packed, npad, kpad = _pack(codes, wfmt, dev)
+    bias_pad = _lib.pad_bias(bias, N, npad, dev)
+    fits = _lib.narrow_conv_fits(wfmt, N, C * kh * kw)
+    outs = []
+    prev = _lib.conv_wonly_narrow(1)
+    try:
+        for on in (1, 0):
+            _lib.conv_wonly_narrow(on)
+            outs.append(_lib.conv_wonly(x, (kh, kw), stride, padding, dilation, packed, wfmt, N, npad, kpad, d,
+                                        bias_pad).cpu())
+    finally:
+        _lib.conv_wonly_narrow(prev)
+    panel = (C * kh * kw + 63) // 64 * 16 * ((N + 15) // 16) * (32 if wfmt == _lib.W4 else 64)
+    assert fits == (panel <= 24 * 1024)
+    assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("geo", [NARROW[0], NARROW[1], NARROW[-1], GEOMETRIES[6]], ids=lambda g: "x".join(map(str, g[:7])))
+@pytest.mark.parametrize("a_bit", [4, 2, 7])
+def test_conv_wonly_bn_act_equals_composed(dev, geo, a_bit):
+    """qvit_conv_wonly_bn_act = the conv, then y alpha + shift (an fp32 multiply, then an add) with the
+    ultra_bn_fold coefficients, then the activation quantizer's values (qvit_fake_quant_f32), bit for bit."""
+    B, C, H, W, N, kh, kw, stride, padding, dilation, wfmt = geo
+    g = torch.Generator().manual_seed(N + a_bit)
+    lvl = 7 if wfmt == _lib.W4 else 127
+    codes = torch.randint(-lvl, lvl + 1, (N, C * kh * kw), generator=g)
+    x = (torch.rand(B, C, H, W, generator=g)).to(dev)
+    d = torch.tensor([1.0 / 7], device=dev)
+    packed, npad, kpad = _pack(codes, wfmt, dev)
+    bn = torch.nn.BatchNorm2d(N).eval()
+    with torch.no_grad():
+        bn.running_mean.copy_(torch.randn(N, generator=g) * 2)
+        bn.running_var.copy_(torch.rand(N, generator=g) * 20 + 0.5)
+        bn.weight.copy_(torch.rand(N, generator=g) * 0.3 + 0.1)
+        bn.bias.copy_(torch.rand(N, generator=g) * 0.4 + 0.3)
+    bn = bn.to(dev)
+    alpha, shift = _lib.ultra_bn_fold(bn, dev)
+    n = 2 ** a_bit - 1
+    got = _lib.conv_wonly_bn_act(x, (kh, kw), stride, padding, dilation, packed, wfmt, N, npad, kpad, d, None, alpha,
+                                 shift, n)
+    assert got is not None
+    y = _lib.conv_wonly(x, (kh, kw), stride, padding, dilation, packed, wfmt, N, npad, kpad, d, None)
+    z = y * alpha.view(1, -1, 1, 1)
+    z = z + shift.view(1, -1, 1, 1)
+    want = _lib.fake_quant_f32(z.contiguous(), _lib.QT_ULTRA_ACT, None, None, None, n).reshape(z.shape)
+    assert torch.equal(got, want)
+    assert len(torch.unique(got)) > min(n, 3)
+
+
+def test_conv2d_q_forward_bn_act_fallbacks(dev):
+    """forward_bn_act fuses only eval-mode BN on running statistics and 1..7-bit quantizers, else returns None."""
+    from quantized_vit_amd.quant_ultra import activation_quantize_fn
+    conv = conv2d_Q_fn(4)(8, 16, kernel_size=3, padding=1, bias=False).to(dev)
+    bn = torch.nn.BatchNorm2d(16).to(dev).eval()
+    x = torch.rand(1, 8, 12, 12, device=dev)
+    with torch.no_grad():
+        assert conv.forward_bn_act(x, bn, activation_quantize_fn(4)) is not None
+        assert conv.forward_bn_act(x, bn, activation_quantize_fn(8)) is None
+        assert conv.forward_bn_act(x, bn.train(), activation_quantize_fn(4)) is None
+        wide = conv2d_Q_fn(4)(8, 80, kernel_size=3, padding=1, bias=False).to(dev)
+        assert wide.forward_bn_act(x, torch.nn.BatchNorm2d(80).to(dev).eval(), activation_quantize_fn(4)) is None
 
 
 def test_conv_wonly_non_contiguous_and_rejects(dev):
