@@ -198,23 +198,6 @@ int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda,
               int out_levels, const void* epi_table, hipStream_t stream);
 
 /*
- * qvit_gemm for QVIT_EPI_F32 / QVIT_EPI_F32_RESID with a stream-K tail (the residual GEMMs Attention.proj and
- * Mlp.fc2 of vit_model.py:151,175 + Block.forward's residual adds :206-207): the tiles of each XCD's last,
- * partial round (N = 768 gives 1182 tiles for 512 resident workgroups: 2.31 rounds) are split along K into parts
- * of >= 2 stages, one per otherwise idle workgroup; the parts' int32 partials meet in `workspace` and the part
- * that arrives last adds them and runs the epilogue. Integer sums: bit-identical to qvit_gemm.
- *   workspace : device buffer, 256-byte aligned, >= qvit_gemm_sk_workspace_bytes(M, K, lda, npad, wfmt) bytes,
- *               ALL ZERO before the first launch that uses it (each launch leaves its arrival counters zero again);
- *               launches that may overlap (other streams) need workspaces of their own.
- * Other arguments and error codes as qvit_gemm (QVIT_EINVAL for another epilogue or a short workspace).
- */
-int qvit_gemm_sk(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int wfmt, int64_t N,
-                 int64_t npad, const float* d_act, const float* d_wt, const float* bias, int epilogue, void* C,
-                 int64_t ldc, void* workspace, int64_t workspace_bytes, hipStream_t stream);
-/* bytes of qvit_gemm_sk's workspace for these shapes on the current device (0 for invalid arguments) */
-int64_t qvit_gemm_sk_workspace_bytes(int64_t M, int64_t K, int64_t lda, int64_t npad, int wfmt);
-
-/*
  * QVIT_ACT_T32: activation codes in the operand order of the int8 32x32x32 matrix instruction, the input of
  * qvit_gemm_a32. An [M][kpad] code matrix (kpad % 64 == 0) is stored as 1-KiB blocks of 32 rows x 32 columns,
  * block (r / 32, c / 32) at byte (r / 32 * kpad / 32 + c / 32) * 1024; inside it, 16-byte group
@@ -279,16 +262,16 @@ int qvit_conv_wonly(const float* X, int64_t B, int64_t C, int64_t H, int64_t W, 
                     const float* d_wt, const float* bias, float* Y, float* workspace, int64_t workspace_bytes,
                     hipStream_t stream);
 /* N <= 64 output channels with QVIT_W4 / QVIT_W8 codes whose first ceil(C kh kw / 64) stages of 16 ceil(N / 16)
- * rows take at most 24 KiB run the narrow schedule (all weights LDS-resident, no workspace used); bit-identical to
- * the wide one. qvit_conv_wonly_narrow(0 / 1) turns it off / on for the process (-1: query); returns the previous
- * setting. */
+ * rows take at most 24 KiB (and C kh kw <= 1024, H, W < 32767) run the narrow schedule: weights and a tap-offset
+ * table LDS-resident, every wave on its own 16-pixel tiles, no workspace used; bit-identical to the wide one.
+ * qvit_conv_wonly_narrow(0 / 1) turns it off / on for the process (-1: query); returns the previous setting. */
 int qvit_conv_wonly_narrow(int enable);
 
 /*
  * Conv2d_Q -> BatchNorm2d (eval, running statistics) -> activation_quantize_fn in one launch (UltraNet's blocks,
  * reference mymodel.py:71-124 run module by module; quant_ultra.py:59-73, :76-91):
- *   Y = round(clamp(y * bn_alpha[n] + bn_shift[n], 0, 1) * a_levels) / a_levels,  y = qvit_conv_wonly's value
- *   (fp32 multiply, then add: the fold qvit_ultra_bn_fold computes; IEEE division by a_levels = 2^a_bit - 1).
+ *   Y = round(clamp(fma(y, bn_alpha[n], bn_shift[n]), 0, 1) * a_levels) / a_levels,  y = qvit_conv_wonly's value
+ *   (one fused multiply-add with the fold qvit_ultra_bn_fold computes; IEEE division by a_levels = 2^a_bit - 1).
  *   Arguments as qvit_conv_wonly; bn_alpha, bn_shift: device float[N]; 1 <= a_levels <= 127.
  * Only for layers on the narrow schedule (QVIT_EINVAL otherwise: run the modules one by one).
  */

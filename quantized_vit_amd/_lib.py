@@ -70,8 +70,6 @@ _SIGNATURES = {
     "qvit_gemm_a32_fits": [_i64, _i32, _i64, _i64, _i32],
     "qvit_gemm_a32": [_c_p, _i64, _i64, _c_p, _i32, _i64, _i64, _c_p, _c_p, _c_p, _i32, _c_p, _i64, _i32, _c_p, _c_p,
                       _c_p, _i32, _c_p, _c_p],
-    "qvit_gemm_sk": [_c_p, _i64, _i64, _i64, _c_p, _i32, _i64, _i64, _c_p, _c_p, _c_p, _i32, _c_p, _i64, _c_p, _i64,
-                     _c_p],
     "qvit_gemm_wonly": [_c_p, _i64, _i64, _i64, _c_p, _i32, _i64, _i64, _c_p, _c_p, _c_p, _i64, _c_p, _i64, _c_p],
     "qvit_conv_wonly": [_c_p, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _c_p, _i32,
                         _i64, _i64, _i64, _c_p, _c_p, _c_p, _c_p, _i64, _c_p],
@@ -103,7 +101,6 @@ _SIGNATURES = {
 }
 # name -> argtypes of the entry points returning int64_t
 INT64_FUNCS = {
-    "qvit_gemm_sk_workspace_bytes": [_i64, _i64, _i64, _i64, _i32],
 }
 STRING_FUNCS = {"qvit_strerror": [_i32], "qvit_version": []}
 EXPORTED_SYMBOLS = sorted(list(_SIGNATURES) + list(INT64_FUNCS) + list(STRING_FUNCS))
@@ -304,38 +301,6 @@ def gemm(A: torch.Tensor, M: int, K: int, packed: torch.Tensor, wfmt: int, N: in
     return C
 
 
-_SK_WS: dict = {}
-
-
-def sk_workspace(device: torch.device, M: int, K: int, lda: int, npad: int, wfmt: int) -> Optional[torch.Tensor]:
-    """The stream-K workspace of qvit_gemm_sk for this device and stream: arrival counters (zero between launches:
-    every launch leaves them zero) + the split tiles' int32 partials. Allocated zeroed once and grown on demand;
-    one per stream, so launches on different streams never share it. None when the library lacks the entry."""
-    lib = load()
-    if not hasattr(lib, "qvit_gemm_sk_workspace_bytes"):
-        return None
-    need = int(lib.qvit_gemm_sk_workspace_bytes(M, K, lda, npad, wfmt))
-    if need <= 0:
-        return None
-    key = (device, torch.cuda.current_stream(device).cuda_stream)
-    ws = _SK_WS.get(key)
-    if ws is None or ws.numel() < need:
-        ws = torch.zeros(need, dtype=torch.uint8, device=device)
-        _SK_WS[key] = ws
-    return ws
-
-
-def gemm_sk(A: torch.Tensor, M: int, K: int, packed: torch.Tensor, wfmt: int, N: int, npad: int, d_act, d_wt,
-            bias_pad: Optional[torch.Tensor], epilogue: int, C: torch.Tensor, workspace: torch.Tensor) -> torch.Tensor:
-    """qvit_gemm for the fp32 epilogues with the stream-K tail (the XCD's last partial round of tiles split along K
-    over every workgroup; bit-identical to qvit_gemm)."""
-    _require_gpu(A, "codes")
-    _check(load().qvit_gemm_sk(_ptr(A), M, K, A.stride(0), _ptr(packed), wfmt, N, npad, _ptr(d_act), _ptr(d_wt),
-                               _ptr(bias_pad), epilogue, _ptr(C), C.stride(0), _ptr(workspace), workspace.numel(),
-                               _stream(A.device)), "qvit_gemm_sk")
-    return C
-
-
 def t32_rows(M: int) -> int:
     """Rows a QVIT_ACT_T32 code buffer holds for M rows (whole 64-row wave tiles of qvit_gemm_a32)."""
     return (M + 63) // 64 * 64
@@ -415,9 +380,11 @@ def gemm_wonly(X: torch.Tensor, M: int, K: int, packed: torch.Tensor, wfmt: int,
 
 
 def conv_wonly(x: torch.Tensor, kernel_size, stride, padding, dilation, packed: torch.Tensor, wfmt: int, N: int,
-               npad: int, kpad: int, d_wt: torch.Tensor, bias_pad: Optional[torch.Tensor]) -> torch.Tensor:
+               npad: int, kpad: int, d_wt: torch.Tensor, bias_pad: Optional[torch.Tensor],
+               split: bool = True) -> torch.Tensor:
     """F.conv2d(x, d_wt * codes, bias) (groups 1, zero padding) with fp32 NCHW x on qvit_conv_wonly: an implicit
-    GEMM against the packed codes ([N][C kh kw] in the weight's flattening order). Returns NCHW fp32."""
+    GEMM against the packed codes ([N][C kh kw] in the weight's flattening order). Returns NCHW fp32. Few output
+    pixels on the wide schedule split K through a workspace (split=False: never)."""
     _require_gpu(x, "activations")
     if x.dtype != torch.float32 or not x.is_contiguous():
         x = x.float().contiguous()
@@ -427,7 +394,7 @@ def conv_wonly(x: torch.Tensor, kernel_size, stride, padding, dilation, packed: 
     OW = (W + 2 * pw - dw * (kw - 1) - 1) // sw + 1
     y = torch.empty((B, N, OH, OW), dtype=torch.float32, device=x.device)
     M = B * OH * OW
-    small = (npad // 256) * ((M + 63) // 64) < 128 and not narrow_conv_fits(wfmt, N, C * kh * kw)  # (no split)
+    small = split and (npad // 256) * ((M + 63) // 64) < 128 and not narrow_conv_fits(wfmt, N, C * kh * kw, H, W)
     ws = wonly_workspace(x.device, M, npad) if small else None
     _check(load().qvit_conv_wonly(_ptr(x), B, C, H, W, kh, kw, sh, sw, ph, pw, dh, dw, _ptr(packed), wfmt, N, npad,
                                   kpad, _ptr(d_wt), _ptr(bias_pad), _ptr(y), _ptr(ws),
@@ -444,7 +411,7 @@ def conv_wonly_bn_act(x: torch.Tensor, kernel_size, stride, padding, dilation, p
     the caller runs the modules one by one."""
     _require_gpu(x, "activations")
     (kh, kw), (sh, sw), (ph, pw), (dh, dw) = kernel_size, stride, padding, dilation
-    if not narrow_conv_fits(wfmt, N, x.shape[1] * kh * kw):
+    if not narrow_conv_fits(wfmt, N, x.shape[1] * kh * kw, x.shape[2], x.shape[3]):
         return None
     if x.dtype != torch.float32 or not x.is_contiguous():
         x = x.float().contiguous()
@@ -459,15 +426,18 @@ def conv_wonly_bn_act(x: torch.Tensor, kernel_size, stride, padding, dilation, p
 
 
 NARROW_W_MAX = 24 * 1024   # gemm_wonly.hip NW_WMAX: the narrow schedule's LDS weight panel
+NARROW_K_MAX = 1024        # gemm_wonly.hip NW_KMAX: its tap table
 
 
-def narrow_conv_fits(wfmt: int, N: int, kreal: int) -> bool:
+def narrow_conv_fits(wfmt: int, N: int, kreal: int, H: int = 0, W: int = 0) -> bool:
     """Whether qvit_conv_wonly runs the narrow schedule (gemm_wonly.hip narrow_geo): N <= 64 channels, int4 / int8
-    codes, the K stages up to C kh kw of 16 ceil(N / 16) rows within NARROW_W_MAX, the schedule enabled."""
-    if N > 64 or wfmt not in (W4, W8) or not conv_wonly_narrow(-1):
+    codes, the K stages up to C kh kw (<= NARROW_K_MAX taps) of 16 ceil(N / 16) rows within NARROW_W_MAX, input
+    sides below 32767, the schedule enabled."""
+    if N > 64 or wfmt not in (W4, W8) or not conv_wonly_narrow(-1) or H >= 32767 or W >= 32767:
         return False
     nke = (kreal + 63) // 64
-    return nke * 16 * ((N + 15) // 16) * (32 if wfmt == W4 else 64) <= NARROW_W_MAX
+    return (nke * 64 <= NARROW_K_MAX
+            and nke * 16 * ((N + 15) // 16) * (32 if wfmt == W4 else 64) <= NARROW_W_MAX)
 
 
 def conv_wonly_narrow(enable: int = -1) -> bool:

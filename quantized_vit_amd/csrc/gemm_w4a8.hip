@@ -112,13 +112,7 @@ struct EpiArgs {
   int64_t ln_ldc;
   int ln_kpad;
   int* ln_cnt;             // arrivals per 128-row block (zeroed by qvit_gemm_resid_ln before the launch)
-  // stream-K tail (qvit_gemm_sk, fp32 epilogues): arrival counters per tile (zero between launches) and the
-  // int32 partial accumulators of the split tiles, SK_PART_INTS per workgroup
-  int* sk_cnt;
-  int* sk_part;
 };
-
-constexpr int SK_PART_INTS = 256 * 128;   // a 4-wave workgroup's accumulators (128 per lane)
 
 // ---- code table of the int8 epilogues --------------------------------------------------------------
 // The epilogue's output code as a function of its fp32 pre-activation v = alpha*acc + bias,
@@ -249,43 +243,8 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   const int per = ntiles >> 3, rem = ntiles & 7;
   const int lo = xcd * per + (xcd < rem ? xcd : rem);
   const int hi = lo + per + (xcd < rem ? 1 : 0);
-  const int nk = K / BK;  // even, >= 2
-  // ---- stream-K tail (fp32 epilogues, with a workspace): the XCD's tiles past its last whole round (fewer than
-  // team) are split along K into P parts of >= 2 stages, one unit per workgroup slot, so every slot finishes within
-  // a fraction of a tile of the others instead of a third of the slots running one tile more. The parts' int32
-  // partials meet in the workspace; the part whose arrival comes last adds the others' to its accumulators and runs
-  // the tile's epilogue (integer sums: the results are bit-identical to the unsplit tile).
-  constexpr bool SK = (EPI == QVIT_EPI_F32 || EPI == QVIT_EPI_F32_RESID);
-  int reg_end = hi, P = 1, tail0 = hi;
-  if (SK && ep.sk_cnt != nullptr) {
-    const int ntx = hi - lo, rounds = ntx / team, tail = ntx - rounds * team;
-    if (tail > 0) {
-      int pp = team / tail;
-      pp = pp < nk / 2 ? pp : nk / 2;
-      if (pp >= 2) {
-        P = pp;
-        tail0 = lo + rounds * team;
-        reg_end = tail0;
-      }
-    }
-  }
-  const int nreg = (lo + slot < reg_end) ? (reg_end - lo - slot + team - 1) / team : 0;
-  const int nunits = nreg + ((P > 1 && slot < (hi - tail0) * P) ? 1 : 0);
-  if (nunits == 0) return;
-  // unit i of this slot: whole tile lo + slot + i team, or (i == nreg) part slot % P of tail tile tail0 + slot / P,
-  // stages [kb, kb + ku) (even bounds)
-  const int sk_part_i = __builtin_amdgcn_readfirstlane(slot % P);
-  const int sk_tile = __builtin_amdgcn_readfirstlane(tail0 + slot / P);
-  const int sk_kb = __builtin_amdgcn_readfirstlane(2 * ((sk_part_i * (nk >> 1)) / P));
-  const int sk_ku = __builtin_amdgcn_readfirstlane(2 * (((sk_part_i + 1) * (nk >> 1)) / P) - sk_kb);
-  auto unit_of = [&](int i, int& tt, int& kb, int& ku) __attribute__((always_inline)) {
-    const bool reg = i < nreg;
-    tt = reg ? lo + slot + i * team : sk_tile;
-    kb = reg ? 0 : sk_kb;
-    ku = reg ? nk : sk_ku;
-  };
-  int t, kb, ku;
-  unit_of(0, t, kb, ku);
+  int t = lo + slot;
+  if (t >= hi) return;
 
   // epilogue scalars and the code table are set up before the main loop
   // W4 accumulators hold 16 acc exactly: the float epilogues fold the 1/16 into alpha, which gives the very
@@ -316,6 +275,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   // weights: the packed (tile_n, stage) tile is the LDS image itself, staged as contiguous 1-KiB pieces
   constexpr int WROWS_PER_PIECE = 1024 / G::WROW;
   constexpr int WROWS_PER_WAVE = BN / G::NWAVES;
+  const int nk = K / BK;  // even, >= 2
   // a tile's sources are uniform (m0, weight-tile base); the per-lane parts are tile-invariant
   // byte offsets from the A / Wp kernel arguments fit 32 bits (checked by the launcher)
   // LEAN (the fp32 / int32 epilogues): the per-lane parts of a tile's DMA sources (activation rows, clamped at
@@ -528,25 +488,23 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
 
   // prologue: the first tile's stages 0 and 1 (the Src values are scoped to one tile: nothing of them is
   // carried across a loop iteration)
-  int g = 0;   // global stage counter of this block (ring slot = g % RING)
-  int ui = 0;  // unit index
+  int g = 0;  // global stage counter of this block (ring slot = g % RING)
   {
     uint32_t a0[G::XPIECES];
     lane_offsets(lane_opaque());
     tile_a(t, a0, lane_opaque());
     const uint32_t w0 = tile_w(t);
-    issue(t, w0, a0, kb, 0);
-    issue(t, w0, a0, kb + 1, 1);
+    issue(t, w0, a0, 0, 0);
+    issue(t, w0, a0, 1, 1);
   }
   Frags<WFMT> fa, fb;
   QVIT_STAMP_DECL
   QVIT_LSTAMP_DECL
   for (;;) {
-    const bool has_next = ui + 1 < nunits;
-    int tnext = 0, kbn = 0, kun = 0;
-    if (has_next) unit_of(ui + 1, tnext, kbn, kun);
+    const int tnext = t + team;
+    const bool has_next = tnext < hi;
     const int m0 = (t / nb_n) * BM, n0 = (t % nb_n) * BN;
-    if (ku == 2 || !LEAN) {  // (K = 128: no steady step, the tail's first stage is the tile's first)
+    if (nk == 2 || !LEAN) {  // (K = 128: no steady step, the tail's first stage is the tile's first)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -573,10 +531,10 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     read_frags(g % RING, fa);
     // steady steps kt = 0 .. nk-3: issue this tile's stage kt+2 (the first one peeled: zero accumulators)
     int kt = 0;
-    if (LEAN && ku > 2) {
+    if (LEAN && nk > 2) {
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_sched_barrier(0);
-      issue(t, cw, ca, kb + 2, (g + 2) % RING);
+      issue(t, cw, ca, 2, (g + 2) % RING);
       QVIT_STAMP(1);
       stage_sync<D>();
       QVIT_STAMP(2);
@@ -584,7 +542,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
       QVIT_STAMP(3);
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_sched_barrier(0);
-      issue(t, cw, ca, kb + 3, (g + 3) % RING);
+      issue(t, cw, ca, 3, (g + 3) % RING);
       QVIT_STAMP(1);
       stage_sync<D>();
       QVIT_STAMP(2);
@@ -592,10 +550,10 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
       QVIT_STAMP(3);
       kt = 2;
     }
-    for (; kt < ku - 2; kt += 2) {
+    for (; kt < nk - 2; kt += 2) {
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_sched_barrier(0);
-      issue(t, cw, ca, kb + kt + 2, (g + kt + 2) % RING);
+      issue(t, cw, ca, kt + 2, (g + kt + 2) % RING);
       QVIT_STAMP(1);
       stage_sync<D>();
       QVIT_STAMP(2);
@@ -603,7 +561,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
       QVIT_STAMP(3);
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_sched_barrier(0);
-      issue(t, cw, ca, kb + kt + 3, (g + kt + 3) % RING);
+      issue(t, cw, ca, kt + 3, (g + kt + 3) % RING);
       QVIT_STAMP(1);
       stage_sync<D>();
       QVIT_STAMP(2);
@@ -617,66 +575,19 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     const uint32_t nw = has_next ? tile_w(tnext) : 0u;
     if (has_next) {
       tile_a(tnext, na, lane_opaque());  // (here, not at the tile head: this tile's offsets are dead by now)
-      issue(tnext, nw, na, kbn, (g + ku) % RING);
+      issue(tnext, nw, na, 0, (g + nk) % RING);
       stage_sync<D>();
     } else {
       stage_sync<0>();
     }
-    step_core(fa, fb, (g + ku - 1) % RING, true, std::false_type{});
+    step_core(fa, fb, (g + nk - 1) % RING, true, std::false_type{});
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_sched_barrier(0);
-    if (has_next) issue(tnext, nw, na, kbn + 1, (g + ku + 1) % RING);
+    if (has_next) issue(tnext, nw, na, 1, (g + nk + 1) % RING);
     step_core(fb, fa, 0, false, std::false_type{});
     QVIT_STAMP(3);
     QVIT_LSTAMP(1);
 
-    if constexpr (SK) {
-      if (ui >= nreg) {
-        // stream-K unit (the slot's last): every part stores its raw accumulators (sc1, 16 B per lane and register),
-        // every wave waits for its stores, then one lane adds to the tile's counter (agent scope); the part whose
-        // add returns P - 1 came last: it resets the counter, reads the other parts' partials back with sc1 loads
-        // after a workgroup barrier and runs the epilogue (MI355X_MICROARCH.md inter-workgroup visibility, first
-        // row of the sc1 hand-off table). Part q of tile t lives in partial slot (t - tail0) P + q of the XCD group's team.
-        const int first = (t - tail0) * P;
-        const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(
-            ep.sk_part + (int64_t)xcd * team * SK_PART_INTS, (short)0, team * SK_PART_INTS * 4, 0x00020000);
-        const int mine = __builtin_amdgcn_readfirstlane((first + sk_part_i) * SK_PART_INTS * 4);
-        const int voff = lane_opaque() * 16 + wave * 1024;   // thread tid's 16 B of each 4-KiB register row
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int sr = 0; sr < 8; ++sr)
-            __builtin_amdgcn_raw_buffer_store_b128(acc[r][sr], pr, voff, mine + (r * 8 + sr) * 4096, 16);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        asm volatile("s_barrier" ::: "memory");
-        int* flag = reinterpret_cast<int*>(qp_l);
-        if (tid == 0) {
-          const int old = __hip_atomic_fetch_add(ep.sk_cnt + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const int last = old == P - 1 ? 1 : 0;
-          if (last) __hip_atomic_store(ep.sk_cnt + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          *flag = last;
-        }
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        asm volatile("s_barrier" ::: "memory");
-        if (*flag == 0) break;  // workgroup-uniform: another part finishes the tile
-        for (int q = 0; q < P; ++q) {
-          if (q == sk_part_i) continue;
-          const int other = __builtin_amdgcn_readfirstlane((first + q) * SK_PART_INTS * 4);
-          // (8 loads in flight at a time: the accumulators hold every other register)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            v4i ld[8];
-#pragma unroll
-            for (int sr = 0; sr < 8; ++sr)
-              ld[sr] = __builtin_amdgcn_raw_buffer_load_b128(pr, voff, other + (r * 8 + sr) * 4096, 16);
-#pragma unroll
-            for (int sr = 0; sr < 8; ++sr) acc[r][sr] += ld[sr];
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
-      }
-    }
     if (WFMT == QVIT_W4 && EPI == QVIT_EPI_I32) {  // 16 acc -> acc (exact arithmetic shift)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
@@ -978,11 +889,8 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
       QVIT_STAMP(6);
     }
     if (!has_next) break;
-    g += ku;
-    ++ui;
     t = tnext;
-    kb = kbn;
-    ku = kun;
+    g += nk;
   }
   QVIT_STAMP_FLUSH;
   QVIT_LSTAMP_FLUSH;
@@ -1072,28 +980,10 @@ extern "C" int qvit_epi_table_build(int epilogue, int out_qtype, const float* ou
   return qvit_hip_status(hipGetLastError());
 }
 
-namespace {
-
-// stream-K workspace: [arrival counters, one int32 per tile of a launch chunk, 256-B rounded][int32 partials,
-// SK_PART_INTS per resident workgroup]
-int64_t sk_counter_bytes(int64_t M, int64_t K, int64_t lda, int64_t npad, int wfmt) {
-  const int64_t span = (int64_t)0xFFFFFFFF - K;
-  int64_t rows = span / lda / 128 * 128;
-  rows = rows < M ? rows : M;
-  const int64_t ntiles = (npad / BN) * ((rows + 127) / 128);
-  (void)wfmt;
-  return (ntiles * 4 + 255) / 256 * 256;
-}
-int64_t sk_part_bytes(int wfmt) {
-  const int64_t grid = (int64_t)device_cus() * (wfmt == QVIT_W4 ? 2 : 1) / 8 * 8;
-  return (grid < 8 ? 8 : grid) * SK_PART_INTS * 4;
-}
-
-int gemm_impl(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int wfmt, int64_t N,
-              int64_t npad, const float* d_act, const float* d_wt, const float* bias, int epilogue,
-              void* C, int64_t ldc, int out_qtype, const float* out_d, const float* out_qm,
-              const float* out_t, int out_levels, const void* epi_table, void* workspace, int64_t workspace_bytes,
-              hipStream_t stream) {
+extern "C" int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int wfmt, int64_t N,
+                         int64_t npad, const float* d_act, const float* d_wt, const float* bias, int epilogue,
+                         void* C, int64_t ldc, int out_qtype, const float* out_d, const float* out_qm,
+                         const float* out_t, int out_levels, const void* epi_table, hipStream_t stream) {
   if (!A || !Wp || !C) return QVIT_ENULL;
   if (wfmt != QVIT_W4 && wfmt != QVIT_W8) return QVIT_EINVAL;
   if (M < 0 || K <= 0 || K % KTILE || lda < K || N <= 0 || npad < N || npad % BN) return QVIT_EINVAL;
@@ -1117,41 +1007,9 @@ int gemm_impl(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp
   if (epi_table && (((uintptr_t)epi_table) & 15)) return QVIT_EALIGN;
   EpiArgs ep{d_act, d_wt, bias, out_qtype, out_d, out_qm, out_t, out_levels,
              (i8out ? reinterpret_cast<const int8_t*>(epi_table) : nullptr), 1, 1.f, 1.f, nullptr};
-  if (workspace != nullptr && (epilogue == QVIT_EPI_F32 || epilogue == QVIT_EPI_F32_RESID)) {
-    if (((uintptr_t)workspace) & 255) return QVIT_EALIGN;
-    const int64_t cb = sk_counter_bytes(M, K, lda, npad, wfmt);
-    if (workspace_bytes < cb + sk_part_bytes(wfmt)) return QVIT_EINVAL;
-    ep.sk_cnt = reinterpret_cast<int*>(workspace);
-    ep.sk_part = reinterpret_cast<int*>(reinterpret_cast<int8_t*>(workspace) + cb);
-  }
   if (wfmt == QVIT_W4) return dispatch_epi<QVIT_W4>(epilogue, A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
   return dispatch_epi<QVIT_W8>(epilogue, A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
 }
-
-}  // namespace
-
-extern "C" int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int wfmt, int64_t N,
-                         int64_t npad, const float* d_act, const float* d_wt, const float* bias, int epilogue,
-                         void* C, int64_t ldc, int out_qtype, const float* out_d, const float* out_qm,
-                         const float* out_t, int out_levels, const void* epi_table, hipStream_t stream) {
-  return gemm_impl(A, M, K, lda, Wp, wfmt, N, npad, d_act, d_wt, bias, epilogue, C, ldc, out_qtype, out_d, out_qm,
-                   out_t, out_levels, epi_table, nullptr, 0, stream);
-}
-
-extern "C" int64_t qvit_gemm_sk_workspace_bytes(int64_t M, int64_t K, int64_t lda, int64_t npad, int wfmt) {
-  if (M <= 0 || K <= 0 || lda < K || npad <= 0 || (wfmt != QVIT_W4 && wfmt != QVIT_W8)) return 0;
-  return sk_counter_bytes(M, K, lda, npad, wfmt) + sk_part_bytes(wfmt);
-}
-
-extern "C" int qvit_gemm_sk(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int wfmt, int64_t N,
-                            int64_t npad, const float* d_act, const float* d_wt, const float* bias, int epilogue,
-                            void* C, int64_t ldc, void* workspace, int64_t workspace_bytes, hipStream_t stream) {
-  if (!workspace) return QVIT_ENULL;
-  if (epilogue != QVIT_EPI_F32 && epilogue != QVIT_EPI_F32_RESID) return QVIT_EINVAL;
-  return gemm_impl(A, M, K, lda, Wp, wfmt, N, npad, d_act, d_wt, bias, epilogue, C, ldc, 0, nullptr, nullptr,
-                   nullptr, 0, nullptr, workspace, workspace_bytes, stream);
-}
-
 
 extern "C" int qvit_gemm_resid_ln(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int wfmt,
                                   int64_t N, int64_t npad, const float* d_act, const float* d_wt, const float* bias,

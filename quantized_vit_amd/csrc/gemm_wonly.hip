@@ -324,46 +324,44 @@ __global__ __launch_bounds__(256) void wonly_reduce_kernel(const float* __restri
 
 // ---- narrow convolution (N <= 64 output channels, UltraNet's Conv2d_Q layers) -----------------------------------
 // The wide kernel's 256-row weight tile is 75-94 % padding for 16-64 output channels. Here all N features (NT
-// MFMA tiles of 16) of all K stages sit in LDS for the workgroup's lifetime (loaded once, re-ordered from the
-// packed image so that LDS row f = feature f), and the workgroup walks 64-pixel tiles: wave w computes pixels
-// 16 w .. 16 w + 15 of the tile against the NT feature tiles. The patch gather is transposed too: lane = pixel,
-// wave = 16-tap quarter of the 64-deep stage, so the tap (c, ky, kx) and its input offset are wave-uniform (scalar)
-// and every tap load reads 64 consecutive output pixels' inputs; quarters and stages past C kh kw are skipped.
-// MFMAs, their operands and their order per accumulator (stage, chunk c, bf16 plane p) are the wide kernel's, so
-// the results are bit-identical to it (tests/test_gpu_ultra_modules.py::test_conv_wonly_narrow_equals_wide).
+// MFMA tiles of 16) of all K stages sit in LDS for the workgroup's lifetime (loaded once, re-ordered from the packed
+// image so that LDS row f = feature f), with a table of every tap's input offset, and each WAVE then runs on its own,
+// with no barrier and no LDS staging of the patches: a wave tile is 16 output pixels, lane (fr, fq) gathers the 16
+// consecutive taps 64 st + 16 fq .. + 15 of pixel fr itself (straight into its MFMA operand registers, split into
+// the three bf16 terms there), and the wave walks its tiles with the next (tile, stage)'s taps loaded while the
+// current one computes. MFMAs, their operands and their order per accumulator (stage, chunk c, bf16 term p) are the
+// wide kernel's, so the results are bit-identical to it (tests/test_gpu_ultra_modules.py::
+// test_conv_wonly_narrow_equals_wide). Stages past C kh kw are skipped.
 // EPI 0: y = (d_w / s) acc + bias; EPI 1 (qvit_conv_wonly_bn_act, Conv2d_Q -> BatchNorm2d(eval) ->
-// activation_quantize_fn): z = y alpha_n + shift_n (fp32 multiply, then add: the fold ultra_bn_fold computes)
-// -> round(clamp(z, 0, 1) levels) / levels.
-constexpr int NW_BM = 64;                              // pixels per tile
-constexpr int NW_WMAX = 24 * 1024;                     // weight panel bytes (two workgroups per CU)
-constexpr int NW_LDS = 2 * WO_XBYTES + NW_WMAX + 3 * 64 * 4;
-static_assert(2 * NW_LDS <= 163840, "two workgroups per CU");
+// activation_quantize_fn): z = fma(y, alpha_n, shift_n) (one rounding; alpha, shift: the fold ultra_bn_fold computes,
+// the fused network's BN step, whose mul + add the compiler contracts the same way) -> round(clamp(z, 0, 1) levels) /
+// levels.
+constexpr int NW_WMAX = 24 * 1024;                     // weight panel bytes
+constexpr int NW_KMAX = 1024;                          // taps in the offset table (C kh kw <= 1024)
+constexpr int NW_WAVES = 4;
 
 bool g_wonly_narrow = true;
 
 template <int WFMT, int NT, int EPI>
-__global__ __launch_bounds__(256, 2) void conv_wonly_narrow_kernel(
+__global__ __launch_bounds__(NW_WAVES * 64) void conv_wonly_narrow_kernel(
     const float* __restrict__ X, int M, int nke, const int8_t* __restrict__ Wp, int N,
     const float* __restrict__ d_wt, const float* __restrict__ bias, const float* __restrict__ bn_a,
     const float* __restrict__ bn_s, float levels, float* __restrict__ Y, const WoConv cg) {
   using G = WoGeo<WFMT>;
   constexpr int NF = 16 * NT;                          // feature rows held
-  __shared__ __attribute__((aligned(16))) int8_t nw_smem[NW_LDS];
-  int8_t* xs_l = nw_smem;                              // 2 x-stages (3 bf16 planes each)
-  int8_t* w_l = nw_smem + 2 * WO_XBYTES;               // [stage][NF rows][WROW]
-  float* bias_l = reinterpret_cast<float*>(w_l + nke * NF * G::WROW);
-  float* bna_l = bias_l + NF;
-  float* bns_l = bna_l + NF;
+  __shared__ __attribute__((aligned(16))) int8_t w_l[NW_WMAX];    // [stage][NF rows][WROW]
+  __shared__ __attribute__((aligned(16))) int2 tap_l[NW_KMAX];    // tap k: {input offset, dy << 16 | dx}
+  __shared__ float par_l[3][64];                                  // bias, BN alpha, BN shift
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
 
-  // weight panel: LDS row f of stage st = packed row rho(f) (perm_row's inverse inside the first 64-row group),
-  // chunks re-swizzled from rho's position to f's
+  // ---- workgroup setup: weight panel (LDS row f of stage st = packed row rho(f), the inverse of perm_row inside
+  // the first 64-row group, chunks re-swizzled from rho's position to f's), tap table, epilogue parameters
   {
     constexpr int CH = G::WROW / 4;                    // 8 (W4) / 16 (W8) bytes per chunk
     const int units = nke * NF * 4;
-    for (int u = tid; u < units; u += 256) {
+    for (int u = tid; u < units; u += NW_WAVES * 64) {
       const int c = u & 3, f = (u >> 2) % NF, st = (u >> 2) / NF;
       const int rho = 16 * ((f >> 2) & 3) + 4 * (f >> 4) + (f & 3);
       const int sw_src = WFMT == QVIT_W4 ? ((rho >> 3) & 1) << 1 : ((rho >> 2) & 1) << 1;
@@ -373,103 +371,93 @@ __global__ __launch_bounds__(256, 2) void conv_wonly_narrow_kernel(
       if (CH == 8) *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(src);
       else *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
     }
-    for (int f = tid; f < NF; f += 256) {
-      bias_l[f] = (bias && f < N) ? bias[f] : 0.f;
-      if (EPI == 1) {
-        bna_l[f] = f < N ? bn_a[f] : 0.f;
-        bns_l[f] = f < N ? bn_s[f] : 0.f;
+    const int khw = cg.kh * cg.kw;
+    for (int k = tid; k < nke * WO_BK; k += NW_WAVES * 64) {
+      int2 e = make_int2(0, 0x7fff0000);               // past C kh kw: dy out of range (zero tap)
+      if (k < cg.kreal) {
+        const int c = k / khw, r = k - c * khw, ky = r / cg.kw, kx = r - ky * cg.kw;
+        const int dy = ky * cg.dh, dx = kx * cg.dw;
+        e = make_int2((c * cg.H + dy) * cg.W + dx, (dy << 16) | dx);
       }
+      tap_l[k] = e;
+    }
+    for (int f = tid; f < 64; f += NW_WAVES * 64) {
+      par_l[0][f] = (bias && f < N) ? bias[f] : 0.f;
+      par_l[1][f] = (EPI == 1 && f < N) ? bn_a[f] : 0.f;
+      par_l[2][f] = (EPI == 1 && f < N) ? bn_s[f] : 0.f;
     }
   }
+  __syncthreads();
 
-  const int ntiles = (M + NW_BM - 1) / NW_BM;
-  const int my = ntiles > (int)blockIdx.x ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int ntiles = (M + 15) / 16;                    // wave tiles of 16 pixels
+  const int gw = (int)blockIdx.x * NW_WAVES + wave, tw = (int)gridDim.x * NW_WAVES;
+  const int my = ntiles > gw ? (ntiles - 1 - gw) / tw + 1 : 0;
   const int units = my * nke;
-  const int khw = cg.kh * cg.kw;
-
-  // the load side: this lane's pixel of the tile being loaded (lane = pixel, wave = quarter)
+  // the load side: this lane's pixel of the tile being loaded
   int64_t lbase = 0;
   int iy0 = 0, ix0 = 0;
   bool mval = false;
-  auto pixel = [&](int tile) __attribute__((always_inline)) {
-    const int m = tile * NW_BM + lane;
-    mval = m < M;
-    const int mm = mval ? m : M - 1;
-    const int b = mm / cg.L, p = mm - b * cg.L, oy = p / cg.OW;
-    iy0 = oy * cg.sh - cg.ph;
-    ix0 = (p - oy * cg.OW) * cg.sw - cg.pw;
-    lbase = (int64_t)b * cg.C * cg.H * cg.W + (int64_t)iy0 * cg.W + ix0;
-  };
   float xv[16];
   auto load = [&](int u) __attribute__((always_inline)) {
     const int i = u / nke, st = u - i * nke;
-    if (st == 0) pixel((int)blockIdx.x + i * (int)gridDim.x);
-    const int k0 = st * WO_BK + 16 * wave;             // wave-uniform
-    if (k0 >= cg.kreal) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) xv[e] = 0.f;
-      return;
+    if (st == 0) {
+      const int m = (gw + i * tw) * 16 + fr;
+      mval = m < M;
+      const int mm = mval ? m : M - 1;
+      const int b = mm / cg.L, p = mm - b * cg.L, oy = p / cg.OW;
+      iy0 = oy * cg.sh - cg.ph;
+      ix0 = (p - oy * cg.OW) * cg.sw - cg.pw;
+      lbase = (int64_t)b * cg.C * cg.H * cg.W + (int64_t)iy0 * cg.W + ix0;
     }
-    int c = k0 / khw, r = k0 - c * khw, ky = r / cg.kw, kx = r - ky * cg.kw;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      float v = 0.f;
-      if (k0 + e < cg.kreal) {
-        const int dy = ky * cg.dh, dx = kx * cg.dw;
-        const bool ok = mval && (unsigned)(iy0 + dy) < (unsigned)cg.H && (unsigned)(ix0 + dx) < (unsigned)cg.W;
-        const int64_t idx = ok ? lbase + ((int64_t)c * cg.H + dy) * cg.W + dx : 0;
-        v = X[idx];
-        v = ok ? v : 0.f;
-      }
-      xv[e] = v;
-      if (++kx == cg.kw) {
-        kx = 0;
-        if (++ky == cg.kh) {
-          ky = 0;
-          ++c;
-        }
-      }
-    }
-  };
-  auto store = [&](int b) __attribute__((always_inline)) {
-    uint32_t p1[8], p2[8], p3[8];
+    const int2* tp = tap_l + st * WO_BK + 16 * fq;
 #pragma unroll
     for (int e = 0; e < 16; e += 2) {
-      const float a = xv[e], c = xv[e + 1];
-      const float a1 = trunc_bf16(a), c1 = trunc_bf16(c);
-      const float ar = a - a1, cr = c - c1;
-      const float a2 = trunc_bf16(ar), c2 = trunc_bf16(cr);
-      const float a3 = ar - a2, c3 = cr - c2;
-      p1[e >> 1] = hi16(a1, c1);
-      p2[e >> 1] = hi16(a2, c2);
-      p3[e >> 1] = hi16(a3, c3);
+      const int4 t2 = *reinterpret_cast<const int4*>(tp + e);   // taps e, e + 1
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int off = h ? t2.z : t2.x, dd = h ? t2.w : t2.y;
+        const int dy = dd >> 16, dx = dd & 0xffff;
+        const bool ok = mval && (unsigned)(iy0 + dy) < (unsigned)cg.H && (unsigned)(ix0 + dx) < (unsigned)cg.W;
+        float v = 0.f;
+        if (ok) v = X[lbase + off];  // (exec-masked: padding and taps past C kh kw issue no request)
+        xv[e + h] = v;
+      }
     }
-    int8_t* d = xs_l + b * WO_XBYTES + lane * WO_PITCH + 32 * wave;
-    *reinterpret_cast<uint4*>(d) = make_uint4(p1[0], p1[1], p1[2], p1[3]);
-    *reinterpret_cast<uint4*>(d + 16) = make_uint4(p1[4], p1[5], p1[6], p1[7]);
-    *reinterpret_cast<uint4*>(d + WO_PLANE) = make_uint4(p2[0], p2[1], p2[2], p2[3]);
-    *reinterpret_cast<uint4*>(d + WO_PLANE + 16) = make_uint4(p2[4], p2[5], p2[6], p2[7]);
-    *reinterpret_cast<uint4*>(d + 2 * WO_PLANE) = make_uint4(p3[0], p3[1], p3[2], p3[3]);
-    *reinterpret_cast<uint4*>(d + 2 * WO_PLANE + 16) = make_uint4(p3[4], p3[5], p3[6], p3[7]);
   };
 
   const int woff = (WFMT == QVIT_W4) ? fr * G::WROW + ((fq ^ (((fr >> 3) & 1) << 1)) << 3)
                                      : fr * G::WROW + ((fq ^ (((fr >> 2) & 1) << 1)) << 4);
-  const int xoff = (16 * wave + fr) * WO_PITCH + 32 * fq;
   const float alpha = (*d_wt) * (WFMT == QVIT_W4 ? 0.0625f : 1.f);
   f4 acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
 
-  if (units > 0) {
-    load(0);
-    store(0);
-  }
-  __syncthreads();  // (also publishes the weight panel)
+  if (units > 0) load(0);
   for (int u = 0; u < units; ++u) {
     const int i = u / nke, st = u - i * nke;
-    if (u + 1 < units) load(u + 1);
-    const int8_t* base = xs_l + (u & 1) * WO_XBYTES;
+    // this unit's taps as the three exact bf16 terms (the wide kernel's split), chunk c = taps 8 c .. 8 c + 7
+    bf8 xs[3][2];
+    {
+      uint32_t p1[8], p2[8], p3[8];
+#pragma unroll
+      for (int e = 0; e < 16; e += 2) {
+        const float a = xv[e], c = xv[e + 1];
+        const float a1 = trunc_bf16(a), c1 = trunc_bf16(c);
+        const float ar = a - a1, cr = c - c1;
+        const float a2 = trunc_bf16(ar), c2 = trunc_bf16(cr);
+        const float a3 = ar - a2, c3 = cr - c2;
+        p1[e >> 1] = hi16(a1, c1);
+        p2[e >> 1] = hi16(a2, c2);
+        p3[e >> 1] = hi16(a3, c3);
+      }
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        xs[0][c] = __builtin_bit_cast(bf8, make_uint4(p1[4 * c], p1[4 * c + 1], p1[4 * c + 2], p1[4 * c + 3]));
+        xs[1][c] = __builtin_bit_cast(bf8, make_uint4(p2[4 * c], p2[4 * c + 1], p2[4 * c + 2], p2[4 * c + 3]));
+        xs[2][c] = __builtin_bit_cast(bf8, make_uint4(p3[4 * c], p3[4 * c + 1], p3[4 * c + 2], p3[4 * c + 3]));
+      }
+    }
+    if (u + 1 < units) load(u + 1);  // lands while this unit computes
     bf8 wb[NT][2];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -488,18 +476,14 @@ __global__ __launch_bounds__(256, 2) void conv_wonly_narrow_kernel(
       wb[t][1] = __builtin_bit_cast(bf8, make_uint4(h[4], h[5], h[6], h[7]));
     }
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      bf8 xsv[3];
-#pragma unroll
-      for (int p = 0; p < 3; ++p) xsv[p] = *reinterpret_cast<const bf8*>(base + xoff + 16 * c + p * WO_PLANE);
+    for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int p = 0; p < 3; ++p)
 #pragma unroll
-        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[t][c], xsv[p], acc[t], 0, 0, 0);
-    }
+        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[t][c], xs[p][c], acc[t], 0, 0, 0);
     if (st == nke - 1) {
-      // epilogue of tile i: lane (fr, fq) holds features 16 t + 4 fq + j of pixel 16 wave + fr
-      const int m = ((int)blockIdx.x + i * (int)gridDim.x) * NW_BM + 16 * wave + fr;
+      // epilogue of the tile: lane (fr, fq) holds features 16 t + 4 fq + j of pixel fr
+      const int m = (gw + i * tw) * 16 + fr;
       if (m < M) {
         const int b = m / cg.L;
         float* yp = Y + ((int64_t)b * N * cg.L + (m - b * cg.L));
@@ -508,9 +492,9 @@ __global__ __launch_bounds__(256, 2) void conv_wonly_narrow_kernel(
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int n = 16 * t + 4 * fq + j;
-            float y = fmaf(alpha, acc[t][j], bias_l[n]);
+            float y = fmaf(alpha, acc[t][j], par_l[0][n]);
             if (EPI == 1) {
-              const float z = __fadd_rn(__fmul_rn(y, bna_l[n]), bns_l[n]);
+              const float z = fmaf(y, par_l[1][n], par_l[2][n]);
               y = rintf(fminf(fmaxf(z, 0.f), 1.f) * levels) / levels;
             }
             if (n < N) yp[(int64_t)n * cg.L] = y;
@@ -519,23 +503,22 @@ __global__ __launch_bounds__(256, 2) void conv_wonly_narrow_kernel(
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
     }
-    if (u + 1 < units) store((u + 1) & 1);  // the other buffer: its last reader finished a barrier ago
-    __syncthreads();
   }
 }
 
-// the narrow schedule's stage count, LDS bytes and feature tiles, or 0 when it does not apply
+// the narrow schedule's stage count and feature tiles, or 0 when it does not apply
 struct NarrowGeo {
-  int nke, nt, lds;
+  int nke, nt;
 };
-NarrowGeo narrow_geo(int wfmt, int64_t N, int64_t npad, int64_t kreal, int64_t K) {
-  if (!g_wonly_narrow || (wfmt != QVIT_W4 && wfmt != QVIT_W8) || N > 64 || npad < 64) return {0, 0, 0};
+NarrowGeo narrow_geo(int wfmt, int64_t N, int64_t npad, int64_t kreal, int64_t K, int64_t H, int64_t W) {
+  if (!g_wonly_narrow || (wfmt != QVIT_W4 && wfmt != QVIT_W8) || N > 64 || npad < 64) return {0, 0};
+  if (H >= 32767 || W >= 32767) return {0, 0};  // (tap offsets dy, dx packed in 16 bits)
   const int nke = (int)((kreal + WO_BK - 1) / WO_BK);
   const int nt = (int)((N + 15) / 16);
   const int wrow = wfmt == QVIT_W4 ? 32 : 64;
   const int64_t wbytes = (int64_t)nke * 16 * nt * wrow;
-  if (nke < 1 || nke > K / WO_BK || wbytes > NW_WMAX) return {0, 0, 0};
-  return {nke, nt, (int)(2 * WO_XBYTES + wbytes + 3 * 16 * nt * 4)};  // (lds: the bytes used of NW_LDS)
+  if (nke < 1 || nke > K / WO_BK || wbytes > NW_WMAX || nke * WO_BK > NW_KMAX) return {0, 0};
+  return {nke, nt};
 }
 
 template <int EPI>
@@ -549,11 +532,13 @@ int narrow_launch(const NarrowGeo& g, const float* X, int64_t M, const int8_t* w
       n = 256;
     return n;
   }();
-  const int64_t ntiles = (M + NW_BM - 1) / NW_BM;
-  const unsigned grid = (unsigned)std::min<int64_t>(ntiles, 2 * (int64_t)cus);
+  // wave tiles of 16 pixels; resident workgroups (8 per CU), no more than the tiles need
+  const int64_t wtiles = (M + 15) / 16;
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((wtiles + NW_WAVES - 1) / NW_WAVES,
+                                                                         8 * (int64_t)cus));
 #define QVIT_NW(F, T)                                                                                            \
-  hipLaunchKernelGGL((conv_wonly_narrow_kernel<F, T, EPI>), dim3(grid), dim3(256), 0, stream, X, (int)M, g.nke, w, \
-                     (int)N, d_wt, bias, bn_a, bn_s, levels, Y, cg)
+  hipLaunchKernelGGL((conv_wonly_narrow_kernel<F, T, EPI>), dim3(grid), dim3(NW_WAVES * 64), 0, stream, X, (int)M, \
+                     g.nke, w, (int)N, d_wt, bias, bn_a, bn_s, levels, Y, cg)
 #define QVIT_NW_T(F)      \
   switch (g.nt) {         \
     case 1: QVIT_NW(F, 1); break; \
@@ -579,7 +564,7 @@ int wonly_launch(const float* X, int64_t M, int64_t K, int64_t ldx, const void* 
   const int64_t ntiles = (npad / WO_BN) * ((M + WO_BM - 1) / WO_BM);
   if (ntiles > INT32_MAX / 2) return QVIT_EINVAL;
   if (CONV) {  // few output channels: the narrow schedule
-    const NarrowGeo g = narrow_geo(wfmt, N, npad, cg.kreal, K);
+    const NarrowGeo g = narrow_geo(wfmt, N, npad, cg.kreal, K, cg.H, cg.W);
     if (g.nke > 0)
       return narrow_launch<0>(g, X, M, reinterpret_cast<const int8_t*>(Wp), wfmt, N, d_wt, bias, nullptr, nullptr,
                               0.f, Y, cg, stream);
@@ -684,7 +669,7 @@ extern "C" int qvit_conv_wonly_bn_act(const float* X, int64_t B, int64_t C, int6
   if (st != QVIT_OK) return st;
   if (!bn_alpha || !bn_shift) return QVIT_ENULL;
   if (a_levels < 1 || a_levels > 127) return QVIT_EINVAL;
-  const NarrowGeo g = narrow_geo(wfmt, N, npad, cg.kreal, K);
+  const NarrowGeo g = narrow_geo(wfmt, N, npad, cg.kreal, K, cg.H, cg.W);
   if (g.nke == 0) return QVIT_EINVAL;  // (N > 64, W16 / W24, or a weight panel past NW_WMAX: unfused modules)
   if (M == 0) return QVIT_OK;
   return narrow_launch<1>(g, X, M, reinterpret_cast<const int8_t*>(Wp), wfmt, N, d_wt, bias, bn_alpha, bn_shift,

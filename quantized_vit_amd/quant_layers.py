@@ -25,7 +25,6 @@ from __future__ import annotations
 
 import logging
 import math
-import os
 import warnings
 from dataclasses import dataclass, field
 from enum import Enum
@@ -39,10 +38,6 @@ import torch.nn.functional as F
 from . import _lib
 
 logger = logging.getLogger(__name__)
-
-# The fp32 epilogues (the residual GEMMs proj / fc2, plain EPI_F32 layers) run with the stream-K tail (qvit_gemm_sk:
-# the last partial round of tiles split along K over every workgroup; bit-identical). QVIT_STREAM_K=0 turns it off.
-STREAM_K = os.environ.get("QVIT_STREAM_K", "1") != "0"
 
 
 class NanInGradientError(Exception):
@@ -442,12 +437,6 @@ class QuantizeMixin:
                 out = torch.empty((M, _round_up(plan.n, 4)), dtype=torch.int32, device=dev)
         elif out is None:
             out = torch.empty((M, _round_up(plan.n, 4)), dtype=torch.float32, device=dev)
-        if STREAM_K and epilogue in (_lib.EPI_F32, _lib.EPI_F32_RESID):
-            ws = _lib.sk_workspace(dev, M, plan.kpad, codes.stride(0), plan.npad, plan.wfmt)
-            if ws is not None:
-                _lib.gemm_sk(codes, M, plan.kpad, plan.packed, plan.wfmt, plan.n, plan.npad, plan.d_act, plan.d_wt,
-                             plan.bias_pad, epilogue, out, ws)
-                return out
         _lib.gemm(codes, M, plan.kpad, plan.packed, plan.wfmt, plan.n, plan.npad, plan.d_act, plan.d_wt,
                   plan.bias_pad, epilogue, out, **oq)
         return out

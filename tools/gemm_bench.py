@@ -30,8 +30,6 @@ SHAPES = {
     "fc1_i8": (M_B256, 3072, 768, _lib.EPI_I8),
     "fc1_i8nt": (M_B256, 3072, 768, _lib.EPI_I8),   # no code table: per-element quantizer
     "fc2": (M_B256, 768, 3072, _lib.EPI_F32_RESID),
-    "fc2_sk": (M_B256, 768, 3072, _lib.EPI_F32_RESID),   # qvit_gemm_sk: the stream-K tail
-    "proj_sk": (M_B256, 768, 768, _lib.EPI_F32_RESID),
     "big": (16384, 8192, 4096, _lib.EPI_I32),
     # proj / fc2 with the next LayerNorm + quantizer behind the tiles (qvit_gemm_resid_ln)
     "proj_ln": (M_B256, 768, 768, -1),
@@ -70,14 +68,11 @@ def run(name, M, N, K, epi, iters, dev, qtype=_lib.QT_NONLINEAR):
         tab = _lib.epi_table_build(_lib.EPI_I8, qtype, kw["out_d"], kw["out_qm"], kw["out_t"], 0, *geo, dev)
 
     A32 = _lib.rows_to_t32(A, K) if name.endswith("a32") else None
-    ws = _lib.sk_workspace(dev, M, K, K, npad, _lib.W4) if name.endswith("_sk") else None
 
     def launch():
         if epi == -1:
             _lib.gemm_resid_ln(A, M, K, packed, _lib.W4, N, npad, d_a, d_w, bias, C, gamma, beta, 1e-6, qtype,
                                kw["out_d"], kw["out_qm"], kw["out_t"], 0, tab, codes, N)
-        elif ws is not None:
-            _lib.gemm_sk(A, M, K, packed, _lib.W4, N, npad, d_a, d_w, bias, epi, C, ws)
         elif name.endswith("a32"):
             _lib.gemm_a32(A32, M, K, packed, _lib.W4, N, npad, d_a, d_w, bias, epi, C, **kw)
         else:

@@ -1,5 +1,15 @@
 set -u
-O=gpurun_out/${OUTD:-r05m}; mkdir -p $O; export TMPDIR=/tmp
+O=gpurun_out/${OUTD:-r05n}; mkdir -p $O; export TMPDIR=/tmp
+# 1. the LDS-expansion variant of the fused qkv + attention kernel: correctness first
+QVIT_LIB=tools/_diag/libqvit_hip_ldsx.so timeout -k 10 400 python -u -m pytest tests/test_gpu_attention.py tests/test_gpu_production.py -k "qkv_attention" -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/t_ldsx.log 2>&1 || { echo "ldsx tests failed"; tail -30 $O/t_ldsx.log; exit 1; }
+echo "ldsx tests: $(tail -1 $O/t_ldsx.log)"
+for r in 1 2; do
+  for L in quantized_vit_amd/libqvit_hip.so tools/_diag/libqvit_hip_nounpack.so tools/_diag/libqvit_hip_ldsx.so; do
+    timeout -k 10 200 python tools/attn_bench.py --fused --split-only --iters 20 --lib $L > $O/att_$(basename $L .so)_$r.log 2>&1 || { echo "attn_bench failed"; tail -5 $O/att_$(basename $L .so)_$r.log; exit 1; }
+    echo "== $(basename $L) $r: $(grep fused $O/att_$(basename $L .so)_$r.log | tr '\n' ' ')"
+  done
+done
+# 2. stream-K + narrow conv tests, SK on/off model A/B
 timeout -k 10 600 python -u -m pytest tests/test_gpu_gemm_sk.py tests/test_gpu_ultra_modules.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/t.log 2>&1 || { echo "tests failed"; tail -40 $O/t.log; exit 1; }
 echo "tests: $(tail -1 $O/t.log)"
 for r in 1 2; do
@@ -10,9 +20,8 @@ for r in 1 2; do
     echo "== model SK=$sk round $r: $(grep '^{' $O/b_${sk}_$r.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["value"]), "img/s", round(d["ms_per_step"], 3), "ms", {k: round(v["launch_us"], 1) for k, v in d["kernels"].items()})')"
   done
 done
+# 3. module-level UltraNet profile
 timeout -k 10 200 python tools/profile_ultra_modules.py > $O/mods.log 2>&1 || { echo "mods failed"; tail -20 $O/mods.log; exit 1; }
 grep -v amdgpu.ids $O/mods.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/rpm -o mods -- python tools/profile_ultra_modules.py > $O/mods_rp.log 2>&1 || { echo "rocprof mods failed"; tail -20 $O/mods_rp.log; exit 1; }
 S=$(find $O/rpm -name "*kernel_stats.csv" | head -1); python tools/kstats.py $S 12
-QVIT_STEP_MARKERS=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/rp -o bench -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline > $O/bench.log 2>&1 || { echo "rocprof bench failed"; tail -20 $O/bench.log; exit 1; }
-T=$(find $O/rp -name "*kernel_trace.csv" | head -1); python tools/kstats.py --split $T 5 40 > $O/split.txt && head -30 $O/split.txt
