@@ -342,7 +342,10 @@ constexpr int NW_WAVES = 4;
 
 bool g_wonly_narrow = true;
 
-template <int WFMT, int NT, int EPI>
+// PAIR (C kh kw <= 32, one stage whose taps 32 .. 63 are all zero, e.g. UltraNet's layer 0): lanes fq = 2, 3 gather
+// a SECOND 16-pixel tile's taps 0 .. 31 instead of zeros, and one v_permlane32_swap per operand register turns the
+// gathered registers into both tiles' operands (upper half zero): half the gather instructions per pixel.
+template <int WFMT, int NT, int EPI, bool PAIR>
 __global__ __launch_bounds__(NW_WAVES * 64) void conv_wonly_narrow_kernel(
     const float* __restrict__ X, int M, int nke, const int8_t* __restrict__ Wp, int N,
     const float* __restrict__ d_wt, const float* __restrict__ bias, const float* __restrict__ bn_a,
@@ -389,7 +392,8 @@ __global__ __launch_bounds__(NW_WAVES * 64) void conv_wonly_narrow_kernel(
   }
   __syncthreads();
 
-  const int ntiles = (M + 15) / 16;                    // wave tiles of 16 pixels
+  constexpr int TPU = PAIR ? 2 : 1;                    // 16-pixel tiles per unit
+  const int ntiles = (M + 16 * TPU - 1) / (16 * TPU);  // wave units
   const int gw = (int)blockIdx.x * NW_WAVES + wave, tw = (int)gridDim.x * NW_WAVES;
   const int my = ntiles > gw ? (ntiles - 1 - gw) / tw + 1 : 0;
   const int units = my * nke;
@@ -401,7 +405,7 @@ __global__ __launch_bounds__(NW_WAVES * 64) void conv_wonly_narrow_kernel(
   auto load = [&](int u) __attribute__((always_inline)) {
     const int i = u / nke, st = u - i * nke;
     if (st == 0) {
-      const int m = (gw + i * tw) * 16 + fr;
+      const int m = ((gw + i * tw) * TPU + (PAIR ? fq >> 1 : 0)) * 16 + fr;
       mval = m < M;
       const int mm = mval ? m : M - 1;
       const int b = mm / cg.L, p = mm - b * cg.L, oy = p / cg.OW;
@@ -409,7 +413,7 @@ __global__ __launch_bounds__(NW_WAVES * 64) void conv_wonly_narrow_kernel(
       ix0 = (p - oy * cg.OW) * cg.sw - cg.pw;
       lbase = (int64_t)b * cg.C * cg.H * cg.W + (int64_t)iy0 * cg.W + ix0;
     }
-    const int2* tp = tap_l + st * WO_BK + 16 * fq;
+    const int2* tp = tap_l + st * WO_BK + 16 * (PAIR ? fq & 1 : fq);
 #pragma unroll
     for (int e = 0; e < 16; e += 2) {
       const int4 t2 = *reinterpret_cast<const int4*>(tp + e);   // taps e, e + 1
@@ -428,15 +432,17 @@ __global__ __launch_bounds__(NW_WAVES * 64) void conv_wonly_narrow_kernel(
   const int woff = (WFMT == QVIT_W4) ? fr * G::WROW + ((fq ^ (((fr >> 3) & 1) << 1)) << 3)
                                      : fr * G::WROW + ((fq ^ (((fr >> 2) & 1) << 1)) << 4);
   const float alpha = (*d_wt) * (WFMT == QVIT_W4 ? 0.0625f : 1.f);
-  f4 acc[NT];
+  f4 acc[TPU][NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int q = 0; q < TPU; ++q)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[q][t] = f4{0.f, 0.f, 0.f, 0.f};
 
   if (units > 0) load(0);
   for (int u = 0; u < units; ++u) {
     const int i = u / nke, st = u - i * nke;
     // this unit's taps as the three exact bf16 terms (the wide kernel's split), chunk c = taps 8 c .. 8 c + 7
-    bf8 xs[3][2];
+    bf8 xs[3][2], xt[PAIR ? 3 : 1][2];
     {
       uint32_t p1[8], p2[8], p3[8];
 #pragma unroll
@@ -450,11 +456,33 @@ __global__ __launch_bounds__(NW_WAVES * 64) void conv_wonly_narrow_kernel(
         p2[e >> 1] = hi16(a2, c2);
         p3[e >> 1] = hi16(a3, c3);
       }
+      if constexpr (PAIR) {  // lanes 32 .. 63 hold the second tile: split into {lo, 0} and {hi, 0}
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        xs[0][c] = __builtin_bit_cast(bf8, make_uint4(p1[4 * c], p1[4 * c + 1], p1[4 * c + 2], p1[4 * c + 3]));
-        xs[1][c] = __builtin_bit_cast(bf8, make_uint4(p2[4 * c], p2[4 * c + 1], p2[4 * c + 2], p2[4 * c + 3]));
-        xs[2][c] = __builtin_bit_cast(bf8, make_uint4(p3[4 * c], p3[4 * c + 1], p3[4 * c + 2], p3[4 * c + 3]));
+        for (int c = 0; c < 2; ++c) {
+          uint32_t a1[4], a2[4], a3[4], b1[4], b2[4], b3[4];
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            const auto w1 = __builtin_amdgcn_permlane32_swap(p1[4 * c + d], 0u, false, false);
+            const auto w2 = __builtin_amdgcn_permlane32_swap(p2[4 * c + d], 0u, false, false);
+            const auto w3 = __builtin_amdgcn_permlane32_swap(p3[4 * c + d], 0u, false, false);
+            a1[d] = w1[0]; b1[d] = w1[1];
+            a2[d] = w2[0]; b2[d] = w2[1];
+            a3[d] = w3[0]; b3[d] = w3[1];
+          }
+          xs[0][c] = __builtin_bit_cast(bf8, make_uint4(a1[0], a1[1], a1[2], a1[3]));
+          xs[1][c] = __builtin_bit_cast(bf8, make_uint4(a2[0], a2[1], a2[2], a2[3]));
+          xs[2][c] = __builtin_bit_cast(bf8, make_uint4(a3[0], a3[1], a3[2], a3[3]));
+          xt[0][c] = __builtin_bit_cast(bf8, make_uint4(b1[0], b1[1], b1[2], b1[3]));
+          xt[1][c] = __builtin_bit_cast(bf8, make_uint4(b2[0], b2[1], b2[2], b2[3]));
+          xt[2][c] = __builtin_bit_cast(bf8, make_uint4(b3[0], b3[1], b3[2], b3[3]));
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          xs[0][c] = __builtin_bit_cast(bf8, make_uint4(p1[4 * c], p1[4 * c + 1], p1[4 * c + 2], p1[4 * c + 3]));
+          xs[1][c] = __builtin_bit_cast(bf8, make_uint4(p2[4 * c], p2[4 * c + 1], p2[4 * c + 2], p2[4 * c + 3]));
+          xs[2][c] = __builtin_bit_cast(bf8, make_uint4(p3[4 * c], p3[4 * c + 1], p3[4 * c + 2], p3[4 * c + 3]));
+        }
       }
     }
     if (u + 1 < units) load(u + 1);  // lands while this unit computes
@@ -480,28 +508,36 @@ __global__ __launch_bounds__(NW_WAVES * 64) void conv_wonly_narrow_kernel(
 #pragma unroll
       for (int p = 0; p < 3; ++p)
 #pragma unroll
-        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[t][c], xs[p][c], acc[t], 0, 0, 0);
+        for (int t = 0; t < NT; ++t) {
+          acc[0][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[t][c], xs[p][c], acc[0][t], 0, 0, 0);
+          if constexpr (PAIR)
+            acc[PAIR ? 1 : 0][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[t][c], xt[PAIR ? p : 0][c],
+                                                                            acc[PAIR ? 1 : 0][t], 0, 0, 0);
+        }
     if (st == nke - 1) {
-      // epilogue of the tile: lane (fr, fq) holds features 16 t + 4 fq + j of pixel fr
-      const int m = (gw + i * tw) * 16 + fr;
-      if (m < M) {
-        const int b = m / cg.L;
-        float* yp = Y + ((int64_t)b * N * cg.L + (m - b * cg.L));
+      // epilogue of the unit's tiles: lane (fr, fq) holds features 16 t + 4 fq + j of pixel fr
 #pragma unroll
-        for (int t = 0; t < NT; ++t)
+      for (int q = 0; q < TPU; ++q) {
+        const int m = ((gw + i * tw) * TPU + q) * 16 + fr;
+        if (m < M) {
+          const int b = m / cg.L;
+          float* yp = Y + ((int64_t)b * N * cg.L + (m - b * cg.L));
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int n = 16 * t + 4 * fq + j;
-            float y = fmaf(alpha, acc[t][j], par_l[0][n]);
-            if (EPI == 1) {
-              const float z = fmaf(y, par_l[1][n], par_l[2][n]);
-              y = rintf(fminf(fmaxf(z, 0.f), 1.f) * levels) / levels;
+          for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int n = 16 * t + 4 * fq + j;
+              float y = fmaf(alpha, acc[q][t][j], par_l[0][n]);
+              if (EPI == 1) {
+                const float z = fmaf(y, par_l[1][n], par_l[2][n]);
+                y = rintf(fminf(fmaxf(z, 0.f), 1.f) * levels) / levels;
+              }
+              if (n < N) yp[(int64_t)n * cg.L] = y;
             }
-            if (n < N) yp[(int64_t)n * cg.L] = y;
-          }
-      }
+        }
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+        for (int t = 0; t < NT; ++t) acc[q][t] = f4{0.f, 0.f, 0.f, 0.f};
+      }
     }
   }
 }
@@ -532,13 +568,20 @@ int narrow_launch(const NarrowGeo& g, const float* X, int64_t M, const int8_t* w
       n = 256;
     return n;
   }();
-  // wave tiles of 16 pixels; resident workgroups (8 per CU), no more than the tiles need
-  const int64_t wtiles = (M + 15) / 16;
+  // wave units of 16 (PAIR: 32) pixels; resident workgroups (8 per CU), no more than the units need
+  const bool pair = cg.kreal <= 32;
+  const int64_t wtiles = (M + (pair ? 31 : 15)) / (pair ? 32 : 16);
   const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((wtiles + NW_WAVES - 1) / NW_WAVES,
                                                                          8 * (int64_t)cus));
-#define QVIT_NW(F, T)                                                                                            \
-  hipLaunchKernelGGL((conv_wonly_narrow_kernel<F, T, EPI>), dim3(grid), dim3(NW_WAVES * 64), 0, stream, X, (int)M, \
-                     g.nke, w, (int)N, d_wt, bias, bn_a, bn_s, levels, Y, cg)
+#define QVIT_NW2(F, T, PR)                                                                                        \
+  hipLaunchKernelGGL((conv_wonly_narrow_kernel<F, T, EPI, PR>), dim3(grid), dim3(NW_WAVES * 64), 0, stream, X,      \
+                     (int)M, g.nke, w, (int)N, d_wt, bias, bn_a, bn_s, levels, Y, cg)
+#define QVIT_NW(F, T)     \
+  if (pair) {             \
+    QVIT_NW2(F, T, true); \
+  } else {                \
+    QVIT_NW2(F, T, false); \
+  }
 #define QVIT_NW_T(F)      \
   switch (g.nt) {         \
     case 1: QVIT_NW(F, 1); break; \
@@ -553,6 +596,7 @@ int narrow_launch(const NarrowGeo& g, const float* X, int64_t M, const int8_t* w
   }
 #undef QVIT_NW_T
 #undef QVIT_NW
+#undef QVIT_NW2
   return qvit_hip_status(hipGetLastError());
 }
 
