@@ -113,6 +113,15 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
   const int my_units = (uhi - ulo - slot + team - 1) / team;  // unit j: ulo + slot + j * team
   const int ntile = (N + 15) / 16;
   const int64_t M = (int64_t)B * N;
+  // projection plan. Wave wr (the wave index rotated by unit) owns the token tiles {2 wr, 2 wr + 1}: their q go to
+  // its registers (the 32-query tile it attends), their k, v to the LDS images. Waves wr, wr + 4 share a SIMD, so
+  // with 13 token tiles (N = 193 .. 208, ViT @224) the SIMDs carry 4, 4, 3 and 2 (+ an idle wave's pass) tiles and
+  // the two busiest set the pace. Balanced plan: the second tile of wr = 4 and wr = 5 (tiles 9, 11) is split by
+  // features at the 8-feature chunk boundary of k: the owner computes fragments 0 .. 5 (q and the first half of
+  // k), the otherwise idle wave wr = 7 computes fragments 6 .. 11 (the rest of k and v) of both tiles and writes
+  // them to the images itself. MFMAs per k-step on the busiest SIMD: 48 -> 42.
+  const bool bal = ntile == 13;
+  auto ptile = [&](int wr_, int tt) -> int { return (bal && wr_ == 7) ? (tt ? 11 : 9) : 2 * wr_ + tt; };
 
   // ---- operand sources of a unit ---------------------------------------------------------------------
   // activations: this lane's rows of the wave's two token tiles as 32-bit byte offsets from A (the launcher
@@ -133,7 +142,7 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
     const int wr = (wave + unit) & (FW - 1);
 #pragma unroll
     for (int tt = 0; tt < TPW; ++tt) {
-      int64_t m = (int64_t)b * N + 16 * (2 * wr + tt) + fr;
+      int64_t m = (int64_t)b * N + 16 * ptile(wr, tt) + fr;
       m = m < M ? m : M - 1;  // tokens past the image: rows of the next one (masked); clamp at the end
       sr.a[tt] = (uint32_t)(m * lda) + (uint32_t)(16 * fq);
     }
@@ -204,6 +213,9 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
 #pragma unroll
     for (int tt = 0; tt < TPW; ++tt) tv[tt] = 2 * wr + tt < ntile;
     const int nt = (tv[0] ? 1 : 0) + (tv[1] ? 1 : 0);
+    // projection ranges of the wave's two tiles: 1 all fragments, 2 fragments 0 .. 5, 3 fragments 6 .. 11, 0 none
+    const int pmode = (bal && wr == 7) ? 3 : (bal && (wr == 4 || wr == 5)) ? 2 : (nt == 2) ? 0 : 1;
+    const int prange[TPW] = {pmode == 3 ? 3 : 1, pmode == 0 ? 1 : pmode == 2 ? 2 : pmode == 3 ? 3 : 0};
 
     // ---- 1. projection ---------------------------------------------------------------------------
     // unit head: everything issued before (the previous unit's output stores included) has landed, the
@@ -229,19 +241,23 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
     // two: 2 when both of the wave's token tiles {2 wr, 2 wr + 1} are inside the image, else 1 (the second
     // tile's MFMAs are skipped; N = 197 has 13 tiles). The order inside a k-step is pinned (sched_barrier); the DMA piece and the two
     // activation loads go between the first fragments' MFMAs in that order (the next top's count).
-    auto kstep = [&](auto two, int s, int q) __attribute__((always_inline)) {
+    auto kstep = [&](auto r0, auto r1, int s, int q) __attribute__((always_inline)) {
+      constexpr int R0 = decltype(r0)::value, R1 = decltype(r1)::value;
+      constexpr auto inr = [](int R, int f) constexpr { return R == 1 || (R == 2 && f < 6) || (R == 3 && f >= 6); };
+      constexpr auto used = [=](int f) constexpr { return inr(R0, f) || inr(R1, f); };
+      constexpr int F0 = (R0 == 3 && R1 != 1 && R1 != 2) ? 6 : 0;  // first fragment used
       __builtin_amdgcn_sched_barrier(0);
       if (s > 0) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(TOPCNT) : "memory");
       __builtin_amdgcn_sched_barrier(0);
       sp.mark(7);
       const int rd = (q + WDIST) & 3, rn = (q + 1) & 3;
       const bool more = s + 1 < nk;
-      v4i wc = unpack16(wfr[0]);
+      v4i wc = unpack16(wfr[F0]);
 #pragma unroll
       for (int f = 0; f < 12; ++f) {
-        if (decltype(two)::value >= 1) acc[0][f] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wc, xa[q][0], acc[0][f], 0, 0, 0);
-        if (decltype(two)::value == 2) acc[1][f] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wc, xa[q][1], acc[1][f], 0, 0, 0);
-        if (f < 11) wc = unpack16(wfr[f + 1]);
+        if (inr(R0, f)) acc[0][f] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wc, xa[q][0], acc[0][f], 0, 0, 0);
+        if (inr(R1, f)) acc[1][f] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wc, xa[q][1], acc[1][f], 0, 0, 0);
+        if (f < 11 && used(f + 1)) wc = unpack16(wfr[f + 1]);
         if (more) wfr[f] = wfrag(rn, f);
         if (f == 0) {  // weight k-step s + 3 (past the unit's end: the next unit's 0, 1, 2)
           if (s + WDIST < nk) dma_piece(cur, s + WDIST, rd);
@@ -262,28 +278,31 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
     // with NKC the k-steps of a unit are straight-line code
     // (k-step 0's weight fragments are read inside each variant: values read before the branch would stay
     // live across both of its structurized arms)
-    auto kloop = [&](auto two) __attribute__((always_inline)) {
+    auto kloop = [&](auto r0, auto r1) __attribute__((always_inline)) {
 #pragma unroll
       for (int f = 0; f < 12; ++f) wfr[f] = wfrag(0, f);
       if constexpr (NKC > 0) {
 #pragma unroll
         for (int s = 0; s < NKC; s += 4) {
-          kstep(two, s, 0);
-          kstep(two, s + 1, 1);
-          kstep(two, s + 2, 2);
-          kstep(two, s + 3, 3);
+          kstep(r0, r1, s, 0);
+          kstep(r0, r1, s + 1, 1);
+          kstep(r0, r1, s + 2, 2);
+          kstep(r0, r1, s + 3, 3);
         }
       } else {
         for (int s = 0; s < nk; s += 4) {
-          kstep(two, s, 0);
-          kstep(two, s + 1, 1);
-          kstep(two, s + 2, 2);
-          kstep(two, s + 3, 3);
+          kstep(r0, r1, s, 0);
+          kstep(r0, r1, s + 1, 1);
+          kstep(r0, r1, s + 2, 2);
+          kstep(r0, r1, s + 3, 3);
         }
       }
     };
-    if (nt == 2) kloop(std::integral_constant<int, 2>{});
-    else kloop(std::integral_constant<int, 1>{});  // (a third, MFMA-free variant for nt == 0 spills)
+    using IC1 = std::integral_constant<int, 1>;
+    if (pmode == 0) kloop(IC1{}, IC1{});
+    else if (pmode == 2) kloop(IC1{}, std::integral_constant<int, 2>{});
+    else if (pmode == 3) kloop(std::integral_constant<int, 3>{}, std::integral_constant<int, 3>{});
+    else kloop(IC1{}, std::integral_constant<int, 0>{});  // (a third, MFMA-free variant for nt == 0 spills)
     cur = nxt;
     unit_src(j + 2, nxt);
     sp.mark(9);
@@ -293,7 +312,9 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
     h8 qh[TPW][2], ql[TPW][2];
 #pragma unroll
     for (int tt = 0; tt < TPW; ++tt) {
-      const int row = 16 * (2 * wr + tt) + fr;  // token / key row of the images
+      const int row = 16 * ptile(wr, tt) + fr;  // token / key row of the images
+      const bool pv = ptile(wr, tt) < ntile;     // (the projection's tile: wr = 7's are 9 and 11 when balanced)
+      const bool lo_half = prange[tt] == 1 || prange[tt] == 2, hi_half = prange[tt] == 1 || prange[tt] == 3;
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
         float x[16];
@@ -314,13 +335,17 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
         split8(xa1, hi1, lo1);
         if (p == 0) {
           qh[tt][0] = hi0; ql[tt][0] = lo0; qh[tt][1] = hi1; ql[tt][1] = lo1;
-        } else if (tv[tt]) {
+        } else if (pv) {
           if (p == 1) {
-            *reinterpret_cast<h8*>(kv + koff(row, 2 * fq)) = hi0;
-            *reinterpret_cast<h8*>(kv + koff(row, 2 * fq + 1)) = hi1;
-            *reinterpret_cast<h8*>(kv + IMGF + koff(row, 2 * fq)) = lo0;
-            *reinterpret_cast<h8*>(kv + IMGF + koff(row, 2 * fq + 1)) = lo1;
-          } else {
+            if (lo_half) {  // fragments 4, 5: features 16 fq .. + 7 of k
+              *reinterpret_cast<h8*>(kv + koff(row, 2 * fq)) = hi0;
+              *reinterpret_cast<h8*>(kv + IMGF + koff(row, 2 * fq)) = lo0;
+            }
+            if (hi_half) {  // fragments 6, 7: features 16 fq + 8 .. + 15
+              *reinterpret_cast<h8*>(kv + koff(row, 2 * fq + 1)) = hi1;
+              *reinterpret_cast<h8*>(kv + IMGF + koff(row, 2 * fq + 1)) = lo1;
+            }
+          } else if (hi_half) {
             *reinterpret_cast<h8*>(kv + 2 * IMGF + v32off(row, 32 * fq)) = hi0;
             *reinterpret_cast<h8*>(kv + 2 * IMGF + v32off(row, 32 * fq + 16)) = hi1;
             *reinterpret_cast<h8*>(kv + 3 * IMGF + v32off(row, 32 * fq)) = lo0;
