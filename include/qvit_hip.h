@@ -70,6 +70,8 @@ extern "C" {
 /* ---- GEMM weight storage ---------------------------------------------------------------- */
 #define QVIT_W4 4   /* int4 codes, 8 per uint32 (see qvit_pack_weight for the nibble order) */
 #define QVIT_W8 8   /* int8 codes                                                           */
+#define QVIT_W4R 40 /* qvit_gemm / qvit_gemm_qkv_split only: QVIT_W4 codes in the register-weight image
+                       (qvit_pack_weight_w4r); same results, each wave's weight rows loaded into registers */
 #define QVIT_W16 16 /* qvit_gemm_wonly only: codes |k| <= 32639 as balanced base-256 digits k = 256 h + l, h and l
                        in [-128, 127], two QVIT_W8 images of npad * kpad bytes (h, then l; qvit_pack_weight)  */
 #define QVIT_W24 24 /* the same with three digits k = 65536 a + 256 h + l (|k| < 2^23, e.g. 16-bit layers whose
@@ -148,6 +150,17 @@ int qvit_pack_weight(const float* w, int64_t n, int64_t k, int64_t ldw, int qtyp
                      hipStream_t stream);
 
 /*
+ * The register-weight image (QVIT_W4R) of a QVIT_W4 image from qvit_pack_weight: the same npad * kpad / 2 bytes,
+ * re-ordered so that in every (256-row tile, 64-deep k stage) chunk of 8 KiB the GEMM lane l of wave w finds its
+ * four 8-byte fragments (rows 64 w + 16 r + (l & 15) of the tile, r = 0..3, k bytes 8 (l >> 4) .. + 7 of the
+ * stage) contiguously at byte 2048 w + 32 l. npad % QVIT_TILE_N == 0, kpad % QVIT_TILE_K == 0, kpad <= 65536;
+ * out must not alias packed. qvit_gemm with wfmt QVIT_W4R on it gives the QVIT_W4 results byte for byte (same
+ * accumulation order); it loads each wave's weights straight into registers instead of through LDS.
+ * Replaces nothing in the reference: a second storage form of quantize_weight's codes (quant_layers.py:332-354).
+ */
+int qvit_pack_weight_w4r(const void* packed, int64_t npad, int64_t kpad, void* out, hipStream_t stream);
+
+/*
  * Pads a bias vector to npad floats (zeros past n; bias may be NULL -> all zeros).
  */
 int qvit_pad_bias(const float* bias, int64_t n, float* out, int64_t npad, hipStream_t stream);
@@ -183,7 +196,8 @@ int qvit_layernorm_quant_i8(const float* x, int64_t rows, int64_t cols, int64_t 
  *   A      : int8 codes [M][lda], K valid columns; K % QVIT_TILE_K == 0 (and K <= 65536 for QVIT_W4), lda % 16 == 0,
  *            A 16-byte aligned, columns past the true in-features must be 0 (the quantizers
  *            above write them so).
- *   Wp     : packed weights from qvit_pack_weight (wfmt, npad rows, kpad == K).
+ *   Wp     : packed weights from qvit_pack_weight (wfmt, npad rows, kpad == K), or with wfmt QVIT_W4R the
+ *            qvit_pack_weight_w4r image of a QVIT_W4 one (same results).
  *   N      : true out features (<= npad); outputs for n >= N are not written.
  *   d_act, d_wt : device float[1] scales; bias : device float[npad] (padded) or NULL.
  *   C      : fp32 / int8 / int32 [M][ldc] per epilogue; ldc % 4 == 0 (fp32/int32), % 16 (int8).

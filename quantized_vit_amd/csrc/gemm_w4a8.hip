@@ -79,6 +79,31 @@ struct Geo {
 QVIT_DEV uint32_t nib16_lo(uint32_t p) { return (p << 4) & 0xF0F0F0F0u; }
 QVIT_DEV uint32_t nib16_hi(uint32_t p) { return p & 0xF0F0F0F0u; }
 
+// A lane's 32-B weight slice of a stage as two 16-B register loads from a wave-uniform base (the register-weight
+// path): issued from asm, so the compiler's wait-count model never drains the asm-issued activation DMA for them;
+// the counted stage waits cover them (2 per stage and wave, as the 2 weight DMA pieces they replace)
+QVIT_DEV void ldw32(v4i& a, v4i& b, const void* sbase, uint32_t voff) {
+  asm volatile("global_load_dwordx4 %0, %2, %3\n\t"
+               "global_load_dwordx4 %1, %2, %3 offset:16"
+               : "=&v"(a), "=&v"(b)
+               : "v"(voff), "s"(sbase)
+               : "memory");
+}
+
+// The register-weight image (QVIT_W4R) of a packed QVIT_W4 weight: in every (tile_n, k-stage) chunk of 8 KiB, wave
+// w's 2 KiB hold lane l's four 8-B fragments (rows 64 w + 16 r + (l & 15), logical k-chunk l >> 4, r = 0..3)
+// contiguously at 32 l, so that a wave's weight slice of a stage is two fully coalesced 16-B loads per lane.
+__global__ void pack_w4r_kernel(const int8_t* __restrict__ src, int8_t* __restrict__ dst, int64_t nunits) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= nunits) return;
+  const int64_t c = u >> 10;
+  const int w = (int)(u >> 8) & 3, ln = (int)(u >> 2) & 63, r = (int)u & 3;
+  const int lfr = ln & 15, lfq = ln >> 4;
+  const int row = 64 * w + 16 * r + lfr;
+  *reinterpret_cast<uint2*>(dst + c * 8192 + w * 2048 + ln * 32 + r * 8) =
+      *reinterpret_cast<const uint2*>(src + c * 8192 + row * 32 + ((lfq ^ (((lfr >> 3) & 1) << 1)) << 3));
+}
+
 
 // Wait until at most N of this wave's DMAs are in flight, retire its LDS reads, then barrier.
 // The LDS drain is the builtin (lgkmcnt(0) = 0xC07F on gfx9) so the compiler's wait-count model sees
@@ -189,6 +214,7 @@ template <int WFMT>
 struct Frags {
   v4i x[8];
   uint2 w4[4];  // W4: packed 16 nibbles per lane
+  v4i wq[2];    // W4R: the four fragments as loaded
   v4i w8[4];    // W8: 16 bytes per lane
 };
 
@@ -214,7 +240,11 @@ QVIT_DEV void st_resid(float* dst, float4 o, const float* C0, int M, int64_t ldc
 // one XCD share their activation panels in its L2), block slot s of the XCD walks lo_x + s + i * team.
 // The operand stages form one stream across the block's tiles: the last two steps of a tile issue the
 // DMA of the next tile's first two stages, so the pipeline never drains between tiles.
-template <int WFMT, int EPI, int WM>
+//
+// RW (QVIT_W4R weights): each wave's 64 weight rows are its own, so they come straight into registers (two 16-B
+// loads per stage and lane, one stage ahead of their MFMAs) instead of through an LDS-DMA piece and a fragment
+// read; the activations stay on the LDS-DMA ring (round 5: fc1 -2.6 % in the model, same box).
+template <int WFMT, int EPI, int WM, bool RW>
 __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) void gemm_kernel(
     const int8_t* __restrict__ A, int M, int K, int64_t lda, const int8_t* __restrict__ Wp, int N, int npad,
     void* __restrict__ C, int64_t ldc, EpiArgs ep) {
@@ -227,6 +257,8 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   const float* bias_l = reinterpret_cast<const float*>(smem + G::RING_BYTES + G::EPI_BYTES);
   QParams* qp_l = reinterpret_cast<QParams*>(smem + G::RING_BYTES + G::EPI_BYTES + G::BIAS_BYTES);
   const bool has_bias = (EPI != QVIT_EPI_I32) && ep.bias != nullptr;
+  constexpr bool REGW = RW;
+  static_assert(!RW || (WFMT == QVIT_W4 && WM == 1), "register weights: the W4 4-wave tile");
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -319,11 +351,25 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
 #pragma unroll
     for (int j = 0; j < G::XPIECES; ++j)
       dma16s(abase, a[j], __builtin_amdgcn_readfirstlane(sx + (32 * wave + 16 * j) * BK));
-    const int8_t* wbase = Wp + wt + (uint32_t)kt * G::WBYTES + (uint32_t)(wave * (G::WPIECES * 1024));
-    // (piece j's 1-KiB step rides in the SGPR base: an instruction offset would move the LDS address too)
+    if constexpr (!REGW) {
+      const int8_t* wbase = Wp + wt + (uint32_t)kt * G::WBYTES + (uint32_t)(wave * (G::WPIECES * 1024));
+      // (piece j's 1-KiB step rides in the SGPR base: an instruction offset would move the LDS address too)
 #pragma unroll
-    for (int j = 0; j < G::WPIECES; ++j)
-      dma16s(wbase + j * 1024, wl, __builtin_amdgcn_readfirstlane(sw + (WROWS_PER_WAVE * wave + WROWS_PER_PIECE * j) * G::WROW));
+      for (int j = 0; j < G::WPIECES; ++j)
+        dma16s(wbase + j * 1024, wl, __builtin_amdgcn_readfirstlane(sw + (WROWS_PER_WAVE * wave + WROWS_PER_PIECE * j) * G::WROW));
+    }
+  };
+  // REGW: this wave's weight slice of stage kt -> f.wq (issued one stage ahead of its MFMAs: the stage wait of the
+  // next step, which counts 4 younger operations, covers it)
+  auto issue_w = [&](uint32_t wt, int kt, Frags<WFMT>& f) __attribute__((always_inline)) {
+    if constexpr (REGW) {
+      const int8_t* wbase = Wp + wt + (uint32_t)kt * G::WBYTES + (uint32_t)(wave * (G::WPIECES * 1024));
+      ldw32(f.wq[0], f.wq[1], wbase, (uint32_t)lane_opaque() * 32u);
+    }
+  };
+  // the loads of f.wq have landed (a counted wait above): tied here, so no use of them is scheduled earlier
+  auto pin = [&](Frags<WFMT>& f) __attribute__((always_inline)) {
+    if constexpr (REGW) asm volatile("" : "+v"(f.wq[0]), "+v"(f.wq[1]));
   };
 
   // per-lane fragment offsets inside a stage (set at each tile head; one add per stage moves them to the slot)
@@ -341,12 +387,14 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     const int8_t* sw = sx + XBYTES;
 #pragma unroll
     for (int s = 0; s < 8; ++s) f.x[s] = *reinterpret_cast<const v4i*>(sx + xoff + s * 16 * BK);
+    if constexpr (!REGW) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (WFMT == QVIT_W4)
-        f.w4[r] = *reinterpret_cast<const uint2*>(sw + woff + r * 16 * G::WROW);
-      else
-        f.w8[r] = *reinterpret_cast<const v4i*>(sw + woff + r * 16 * G::WROW);
+      for (int r = 0; r < 4; ++r) {
+        if (WFMT == QVIT_W4)
+          f.w4[r] = *reinterpret_cast<const uint2*>(sw + woff + r * 16 * G::WROW);
+        else
+          f.w8[r] = *reinterpret_cast<const v4i*>(sw + woff + r * 16 * G::WROW);
+      }
     }
   };
 
@@ -358,7 +406,11 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     for (int r = 0; r < 4; ++r) {
       v4i wf;
       if (WFMT == QVIT_W4) {
-        const uint2 p = f.w4[r];
+        uint2 p = f.w4[r];
+        if constexpr (REGW) {
+          const v4i q = f.wq[r >> 1];
+          p = (r & 1) ? make_uint2((uint32_t)q[2], (uint32_t)q[3]) : make_uint2((uint32_t)q[0], (uint32_t)q[1]);
+        }
         wf = v4i{(int)nib16_lo(p.x), (int)nib16_hi(p.x), (int)nib16_lo(p.y), (int)nib16_hi(p.y)};
       } else {
         wf = f.w8[r];
@@ -515,12 +567,13 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     // previous tile's epilogue, so the tile's bias can be DMA'd into its LDS slot (1 KiB, wave 0;
     // older than every later stage DMA, so the counted stage waits cover it)
     QVIT_STAMP(5);
+    const uint32_t cw = tile_w(t);
+    issue_w(cw, 0, fa);  // REGW: stage 0's weights (covered by the first stage wait below the head)
     __builtin_amdgcn_s_waitcnt(0xC07F);
     stage_sync<D>();
     QVIT_STAMP(0);
     QVIT_LSTAMP(0);
     uint32_t ca[G::XPIECES];
-    const uint32_t cw = tile_w(t);
     {
       const int ln = lane_opaque();
       lane_offsets(ln);
@@ -535,16 +588,20 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_sched_barrier(0);
       issue(t, cw, ca, 2, (g + 2) % RING);
+      issue_w(cw, 1, fb);
       QVIT_STAMP(1);
       stage_sync<D>();
+      pin(fa);
       QVIT_STAMP(2);
       step_core(fa, fb, (g + 1) % RING, true, std::true_type{});
       QVIT_STAMP(3);
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_sched_barrier(0);
       issue(t, cw, ca, 3, (g + 3) % RING);
+      issue_w(cw, 2, fa);
       QVIT_STAMP(1);
       stage_sync<D>();
+      pin(fb);
       QVIT_STAMP(2);
       step_core(fb, fa, (g + 2) % RING, true, std::false_type{});
       QVIT_STAMP(3);
@@ -554,16 +611,20 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_sched_barrier(0);
       issue(t, cw, ca, kt + 2, (g + kt + 2) % RING);
+      issue_w(cw, kt + 1, fb);
       QVIT_STAMP(1);
       stage_sync<D>();
+      pin(fa);
       QVIT_STAMP(2);
       step_core(fa, fb, (g + kt + 1) % RING, true, std::false_type{});
       QVIT_STAMP(3);
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_sched_barrier(0);
       issue(t, cw, ca, kt + 3, (g + kt + 3) % RING);
+      issue_w(cw, kt + 2, fa);
       QVIT_STAMP(1);
       stage_sync<D>();
+      pin(fb);
       QVIT_STAMP(2);
       step_core(fb, fa, (g + kt + 2) % RING, true, std::false_type{});
       QVIT_STAMP(3);
@@ -576,14 +637,24 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     if (has_next) {
       tile_a(tnext, na, lane_opaque());  // (here, not at the tile head: this tile's offsets are dead by now)
       issue(tnext, nw, na, 0, (g + nk) % RING);
+      issue_w(cw, nk - 1, fb);
       stage_sync<D>();
+    } else if constexpr (REGW) {
+      issue_w(cw, nk - 1, fb);
+      stage_sync<2>();
     } else {
       stage_sync<0>();
     }
+    pin(fa);
     step_core(fa, fb, (g + nk - 1) % RING, true, std::false_type{});
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_sched_barrier(0);
     if (has_next) issue(tnext, nw, na, 1, (g + nk + 1) % RING);
+    if constexpr (REGW) {  // the last stage's weights (younger: the next tile's stage-1 pieces, if any)
+      if (has_next) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      pin(fb);
+    }
     step_core(fb, fa, 0, false, std::false_type{});
     QVIT_STAMP(3);
     QVIT_LSTAMP(1);
@@ -908,7 +979,7 @@ int device_cus() {
   return cus;
 }
 
-template <int WFMT, int EPI>
+template <int WFMT, int EPI, bool RW = false>
 int launch(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int64_t N, int64_t npad,
            void* C, int64_t ldc, const EpiArgs& ep, hipStream_t stream) {
   constexpr int WMV = 1;   // (a second W4 tile width was measured slower in round 3: DESIGN.md section 8)
@@ -934,7 +1005,7 @@ int launch(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, i
       epc.ln_cnt = ep.ln_cnt + m0 / G::BM;
       epc.ln_codes = ep.ln_codes + m0 * ep.ln_ldc;
     }
-    hipLaunchKernelGGL((gemm_kernel<WFMT, EPI, WMV>), dim3((unsigned)grid), dim3(G::NT), 0, stream, A + m0 * lda,
+    hipLaunchKernelGGL((gemm_kernel<WFMT, EPI, WMV, RW>), dim3((unsigned)grid), dim3(G::NT), 0, stream, A + m0 * lda,
                        (int)mc, (int)K, lda, reinterpret_cast<const int8_t*>(Wp), (int)N, (int)npad, Cc, ldc, epc);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return qvit_hip_status(e);
@@ -942,17 +1013,17 @@ int launch(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, i
   return QVIT_OK;
 }
 
-template <int WFMT>
+template <int WFMT, bool RW = false>
 int dispatch_epi(int epilogue, const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int64_t N,
                  int64_t npad, void* C, int64_t ldc, const EpiArgs& ep, hipStream_t stream) {
   switch (epilogue) {
-    case QVIT_EPI_F32: return launch<WFMT, QVIT_EPI_F32>(A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
-    case QVIT_EPI_F32_RESID: return launch<WFMT, QVIT_EPI_F32_RESID>(A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
-    case QVIT_EPI_I8_GELU: return launch<WFMT, QVIT_EPI_I8_GELU>(A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
-    case QVIT_EPI_I8: return launch<WFMT, QVIT_EPI_I8>(A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
-    case QVIT_EPI_I32: return launch<WFMT, QVIT_EPI_I32>(A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
+    case QVIT_EPI_F32: return launch<WFMT, QVIT_EPI_F32, RW>(A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
+    case QVIT_EPI_F32_RESID: return launch<WFMT, QVIT_EPI_F32_RESID, RW>(A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
+    case QVIT_EPI_I8_GELU: return launch<WFMT, QVIT_EPI_I8_GELU, RW>(A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
+    case QVIT_EPI_I8: return launch<WFMT, QVIT_EPI_I8, RW>(A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
+    case QVIT_EPI_I32: return launch<WFMT, QVIT_EPI_I32, RW>(A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
     case QVIT_EPI_QKV_SPLIT:
-      return launch<WFMT, QVIT_EPI_QKV_SPLIT>(A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
+      return launch<WFMT, QVIT_EPI_QKV_SPLIT, RW>(A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
     default: return QVIT_EINVAL;
   }
 }
@@ -980,15 +1051,26 @@ extern "C" int qvit_epi_table_build(int epilogue, int out_qtype, const float* ou
   return qvit_hip_status(hipGetLastError());
 }
 
+extern "C" int qvit_pack_weight_w4r(const void* packed, int64_t npad, int64_t kpad, void* out, hipStream_t stream) {
+  if (!packed || !out) return QVIT_ENULL;
+  if (npad <= 0 || npad % BN || kpad <= 0 || kpad % KTILE || npad > INT32_MAX / 2 || kpad > 65536) return QVIT_EINVAL;
+  if ((((uintptr_t)packed) & 15) || (((uintptr_t)out) & 15)) return QVIT_EALIGN;
+  if (packed == out) return QVIT_EINVAL;  // not in place
+  const int64_t units = npad * kpad / 16;  // 8-B slices (npad kpad / 2 bytes)
+  hipLaunchKernelGGL(pack_w4r_kernel, dim3((unsigned)((units + 255) / 256)), dim3(256), 0, stream,
+                     reinterpret_cast<const int8_t*>(packed), reinterpret_cast<int8_t*>(out), units);
+  return qvit_hip_status(hipGetLastError());
+}
+
 extern "C" int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int wfmt, int64_t N,
                          int64_t npad, const float* d_act, const float* d_wt, const float* bias, int epilogue,
                          void* C, int64_t ldc, int out_qtype, const float* out_d, const float* out_qm,
                          const float* out_t, int out_levels, const void* epi_table, hipStream_t stream) {
   if (!A || !Wp || !C) return QVIT_ENULL;
-  if (wfmt != QVIT_W4 && wfmt != QVIT_W8) return QVIT_EINVAL;
+  if (wfmt != QVIT_W4 && wfmt != QVIT_W4R && wfmt != QVIT_W8) return QVIT_EINVAL;
   if (M < 0 || K <= 0 || K % KTILE || lda < K || N <= 0 || npad < N || npad % BN) return QVIT_EINVAL;
   if (M > INT32_MAX / 2 || npad > INT32_MAX / 2 || K > (1 << 24)) return QVIT_EINVAL;
-  if (wfmt == QVIT_W4 && K > 65536) return QVIT_EINVAL;  // 16x-scaled int32 accumulation bound
+  if (wfmt != QVIT_W8 && K > 65536) return QVIT_EINVAL;  // 16x-scaled int32 accumulation bound
   if ((lda % 16) || (((uintptr_t)A) & 15) || (((uintptr_t)Wp) & 15)) return QVIT_EALIGN;
   if (epilogue < QVIT_EPI_F32 || epilogue > QVIT_EPI_I32) return QVIT_EINVAL;
   const bool i8out = epilogue == QVIT_EPI_I8 || epilogue == QVIT_EPI_I8_GELU;
@@ -1008,6 +1090,7 @@ extern "C" int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda, con
   EpiArgs ep{d_act, d_wt, bias, out_qtype, out_d, out_qm, out_t, out_levels,
              (i8out ? reinterpret_cast<const int8_t*>(epi_table) : nullptr), 1, 1.f, 1.f, nullptr};
   if (wfmt == QVIT_W4) return dispatch_epi<QVIT_W4>(epilogue, A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
+  if (wfmt == QVIT_W4R) return dispatch_epi<QVIT_W4, true>(epilogue, A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
   return dispatch_epi<QVIT_W8>(epilogue, A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
 }
 
@@ -1048,11 +1131,11 @@ extern "C" int qvit_gemm_qkv_split(const int8_t* A, int64_t M, int64_t K, int64_
                                    int64_t N, int64_t npad, const float* d_act, const float* d_wt, const float* bias,
                                    int64_t seq, float in_scale, void* qkv_hi, void* qkv_lo, hipStream_t stream) {
   if (!A || !Wp || !qkv_hi || !qkv_lo || !d_act || !d_wt) return QVIT_ENULL;
-  if (wfmt != QVIT_W4 && wfmt != QVIT_W8) return QVIT_EINVAL;
+  if (wfmt != QVIT_W4 && wfmt != QVIT_W4R && wfmt != QVIT_W8) return QVIT_EINVAL;
   if (M < 0 || K <= 0 || K % KTILE || lda < K || N <= 0 || N % 64 || npad < N || npad % BN) return QVIT_EINVAL;
   if (M > INT32_MAX / 2 || npad > INT32_MAX / 2 || K > (1 << 24)) return QVIT_EINVAL;
   if (seq <= 0 || seq > (1 << 20) || M % seq || !(in_scale > 0.f)) return QVIT_EINVAL;
-  if (wfmt == QVIT_W4 && K > 65536) return QVIT_EINVAL;
+  if (wfmt != QVIT_W8 && K > 65536) return QVIT_EINVAL;
   if ((lda % 16) || (((uintptr_t)A) & 15) || (((uintptr_t)Wp) & 15)) return QVIT_EALIGN;
   if ((((uintptr_t)qkv_hi) & 15) || (((uintptr_t)qkv_lo) & 15)) return QVIT_EALIGN;
   if (bias && (((uintptr_t)bias) & 15)) return QVIT_EALIGN;
@@ -1061,5 +1144,7 @@ extern "C" int qvit_gemm_qkv_split(const int8_t* A, int64_t M, int64_t K, int64_
              reinterpret_cast<_Float16*>(qkv_lo)};
   if (wfmt == QVIT_W4)
     return launch<QVIT_W4, QVIT_EPI_QKV_SPLIT>(A, M, K, lda, Wp, N, npad, qkv_hi, N, ep, stream);
+  if (wfmt == QVIT_W4R)
+    return launch<QVIT_W4, QVIT_EPI_QKV_SPLIT, true>(A, M, K, lda, Wp, N, npad, qkv_hi, N, ep, stream);
   return launch<QVIT_W8, QVIT_EPI_QKV_SPLIT>(A, M, K, lda, Wp, N, npad, qkv_hi, N, ep, stream);
 }

@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import logging
 import math
+import os
 import warnings
 from dataclasses import dataclass, field
 from enum import Enum
@@ -117,6 +118,12 @@ def _round_up(v: int, m: int) -> int:
     return (v + m - 1) // m * m
 
 
+# The int path's W4 GEMMs (qvit_gemm, qvit_gemm_qkv_split) take the register-weight image of the packed codes
+# (qvit_pack_weight_w4r: same results, each GEMM wave's weight rows loaded into registers instead of through LDS;
+# round 5: fc1 -2.6 % in the model). QVIT_GEMM_W4R=0 keeps the LDS-staged form (same-box A/B).
+GEMM_W4R = os.environ.get("QVIT_GEMM_W4R", "1") == "1"
+
+
 @dataclass
 class QuantPlan:
     """Per-layer device state derived from the parameters (rebuilt when any of them changes)."""
@@ -141,6 +148,11 @@ class QuantPlan:
     qm_act: Optional[torch.Tensor] = None
     t_act: Optional[torch.Tensor] = None
     extra: dict = field(default_factory=dict)
+
+    def gemm_weights(self) -> Tuple[torch.Tensor, int]:
+        """(image, wfmt) the int path's GEMM reads: the W4R image when the plan holds one, else the packed codes."""
+        w4r = self.extra.get("w4r")
+        return (w4r, _lib.W4R) if w4r is not None else (self.packed, self.wfmt)
 
 
 class QuantizeMixin:
@@ -328,6 +340,8 @@ class QuantizeMixin:
                 packed = _lib.pack_weight(w32, qt_pack, d_pack, qm_pack, t_pack, wfmt, npad, kpad, overflow)
                 if int(overflow.item()) == 0:
                     plan.packed, plan.wfmt, plan.int_path = packed, wfmt, True
+                    if wfmt == _lib.W4 and GEMM_W4R:
+                        plan.extra["w4r"] = _lib.pack_weight_w4r(packed, npad, kpad)
                     break
         if not plan.int_path and abs(lw) <= 65536:
             # fp32 activations against the packed weight codes (qvit_gemm_wonly, QuantizeLinear): the weight-only
@@ -437,7 +451,8 @@ class QuantizeMixin:
                 out = torch.empty((M, _round_up(plan.n, 4)), dtype=torch.int32, device=dev)
         elif out is None:
             out = torch.empty((M, _round_up(plan.n, 4)), dtype=torch.float32, device=dev)
-        _lib.gemm(codes, M, plan.kpad, plan.packed, plan.wfmt, plan.n, plan.npad, plan.d_act, plan.d_wt,
+        wimg, wfmt = plan.gemm_weights()
+        _lib.gemm(codes, M, plan.kpad, wimg, wfmt, plan.n, plan.npad, plan.d_act, plan.d_wt,
                   plan.bias_pad, epilogue, out, **oq)
         return out
 

@@ -317,7 +317,8 @@ class Block(nn.Module):
             in_scale = attention_in_scale(p_qkv)
             hi = torch.empty(M * p_qkv.n, dtype=torch.float16, device=x.device)
             lo = torch.empty(M * p_qkv.n, dtype=torch.float16, device=x.device)
-            _lib.gemm_qkv_split(codes, M, p_qkv.kpad, p_qkv.packed, p_qkv.wfmt, p_qkv.n, p_qkv.npad, p_qkv.d_act,
+            wimg, wfmt = p_qkv.gemm_weights()
+            _lib.gemm_qkv_split(codes, M, p_qkv.kpad, wimg, wfmt, p_qkv.n, p_qkv.npad, p_qkv.d_act,
                                 p_qkv.d_wt, p_qkv.bias_pad, N, in_scale, hi, lo)
             codes = torch.empty((M, p_proj.kpad), dtype=torch.int8, device=x.device)
             if p_proj.kpad != a.num_heads * 64:

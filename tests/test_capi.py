@@ -47,6 +47,7 @@ def test_constants_match_header():
     assert int(consts["QVIT_QT_NONLINEAR"]) == _lib.QT_NONLINEAR
     assert int(consts["QVIT_QT_ULTRA_ACT"]) == _lib.QT_ULTRA_ACT
     assert int(consts["QVIT_W4"]) == _lib.W4 and int(consts["QVIT_W8"]) == _lib.W8
+    assert int(consts["QVIT_W4R"]) == _lib.W4R
     for e in ("F32", "F32_RESID", "I8_GELU", "I8", "I32"):
         assert int(consts[f"QVIT_EPI_{e}"]) == getattr(_lib, f"EPI_{e}")
     assert int(consts["QVIT_TILE_N"]) == _lib.TILE_N and int(consts["QVIT_TILE_K"]) == _lib.TILE_K
@@ -74,5 +75,16 @@ def test_argument_validation_without_launch(lib):
     assert lib.qvit_quantize_act_i8(fake, 4, 16, 16, 2, None, None, None, 0, fake, 16, 16, None) == -1
     # weight packing: npad must be a multiple of the tile
     assert lib.qvit_pack_weight(fake, 10, 128, 128, 0, fake, fake, None, 4, fake, 128, 128, None, None) == -1
+    # register-weight image: npad a multiple of the tile, kpad of QVIT_TILE_K and <= 65536, 16-B aligned, not in place
+    other = ctypes.c_void_p(0x2000)
+    assert lib.qvit_pack_weight_w4r(fake, 100, 128, other, None) == -1
+    assert lib.qvit_pack_weight_w4r(fake, 256, 100, other, None) == -1
+    assert lib.qvit_pack_weight_w4r(fake, 256, 65536 + 128, other, None) == -1
+    assert lib.qvit_pack_weight_w4r(fake, 256, 128, ctypes.c_void_p(0x2008), None) == -2
+    assert lib.qvit_pack_weight_w4r(fake, 256, 128, fake, None) == -1
+    assert lib.qvit_pack_weight_w4r(None, 256, 128, other, None) == -3
+    # QVIT_W4R: the int4 accumulation bound applies; the fused residual + LayerNorm GEMM takes W4 / W8 only
+    assert lib.qvit_gemm(fake, 16, 65536 + 128, 65536 + 128, fake, _lib.W4R, 16, 256, fake, fake, None, 0, fake, 16,
+                         0, None, None, None, 0, None, None) == -1
     # zero-size work is a no-op success
     assert lib.qvit_quantize_act_i8(fake, 0, 16, 16, 0, fake, fake, None, 0, fake, 16, 16, None) == 0
