@@ -21,7 +21,7 @@ import re
 import statistics
 import sys
 
-FC1_KERNEL = re.compile(r"gemm_kernel<4, 2, 1>")  # W4 weights, I8_GELU epilogue, 4 waves
+FC1_KERNEL = re.compile(r"gemm_kernel<4, 2, 1(, (true|false))?>")  # W4 weights, I8_GELU epilogue, 4 waves (W4R or not)
 
 
 def top(path, n=25):
