@@ -68,6 +68,11 @@ def run(name, M, N, K, epi, iters, dev, qtype=_lib.QT_NONLINEAR):
         tab = _lib.epi_table_build(_lib.EPI_I8, qtype, kw["out_d"], kw["out_qm"], kw["out_t"], 0, *geo, dev)
 
     A32 = _lib.rows_to_t32(A, K) if name.endswith("a32") else None
+    # the product's form of the int4 weights (quant_layers.GEMM_W4R) when the loaded library has it; random bytes
+    # either way, so no repacking is needed for timing
+    wfmt = _lib.W4
+    if os.environ.get("QVIT_GEMM_W4R", "1") == "1" and hasattr(_lib.load(), "qvit_pack_weight_w4r"):
+        wfmt = _lib.W4R
 
     def launch():
         if epi == -1:
@@ -76,7 +81,7 @@ def run(name, M, N, K, epi, iters, dev, qtype=_lib.QT_NONLINEAR):
         elif name.endswith("a32"):
             _lib.gemm_a32(A32, M, K, packed, _lib.W4, N, npad, d_a, d_w, bias, epi, C, **kw)
         else:
-            _lib.gemm(A, M, K, packed, _lib.W4, N, npad, d_a, d_w, bias, epi, C, **kw)
+            _lib.gemm(A, M, K, packed, wfmt, N, npad, d_a, d_w, bias, epi, C, **kw)
     times = []
     for i in range(iters + 3):
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

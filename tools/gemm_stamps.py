@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--shapes", default="fc1_i32,fc1,qkv,fc2")
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--lib", default="", help="another -DQVIT_GEMM_STAMPS build (path) instead of the default one")
     ap.add_argument("--build-var", nargs="*", default=[],
                     help="NAME=DEF1,DEF2 ...: build tools/_diag/libqvit_hip_NAME.so with those defines")
     ap.add_argument("--bench-var", default="", help="time variant library NAME (see --build-var)")
@@ -68,7 +69,7 @@ def main():
     from quantized_vit_amd import _lib
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import gemm_bench
-    lib = _lib.load(LIB)
+    lib = _lib.load(a.lib or LIB)
     lib.qvit_gemm_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     lib.qvit_gemm_stamps.restype = ctypes.c_int
     dev = torch.device("cuda:0")
