@@ -91,6 +91,12 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
+def _w4r() -> bool:
+    """Whether the int path's W4 GEMMs run on the register-weight image (quant_layers.GEMM_W4R)."""
+    from quantized_vit_amd import quant_layers
+    return quant_layers.GEMM_W4R
+
+
 def _free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -459,7 +465,7 @@ def main():
                    "parallelism": f"dp{world}"}
                   | ({"rehearsal": f"{world} ranks on one device, gloo, logits gathered through the host "
                                    "(QVIT_BENCH_ONE_DEVICE=1; not a scaling measurement)"} if one_device else {}),
-        "roofline": {"bound": "mfma", "kernel": "fc1 gemm_kernel<W4, EPI_I8_GELU>",
+        "roofline": {"bound": "mfma", "kernel": "fc1 gemm_kernel<W4, EPI_I8_GELU" + (", W4R>" if _w4r() else ">"),
                      "achieved": achieved, "peak": INT8_PEAK_TOPS, "unit": "TFLOP/s",
                      "frac": achieved / INT8_PEAK_TOPS, "traffic": traffic,
                      "ops_per_launch": ops, "launch_ms": fc1_ms,
