@@ -91,10 +91,10 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
-def _w4r() -> bool:
-    """Whether the int path's W4 GEMMs run on the register-weight image (quant_layers.GEMM_W4R)."""
+def _wreg() -> str:
+    """The weight image the int path's W4 GEMMs run on (quant_layers.GEMM_WREG): ", W4R>", ", W8R>" or ">"."""
     from quantized_vit_amd import quant_layers
-    return quant_layers.GEMM_W4R
+    return {"w4r": ", W4R>", "w8r": ", W8R>"}.get(quant_layers.GEMM_WREG, ">")
 
 
 def _free_port() -> int:
@@ -465,7 +465,7 @@ def main():
                    "parallelism": f"dp{world}"}
                   | ({"rehearsal": f"{world} ranks on one device, gloo, logits gathered through the host "
                                    "(QVIT_BENCH_ONE_DEVICE=1; not a scaling measurement)"} if one_device else {}),
-        "roofline": {"bound": "mfma", "kernel": "fc1 gemm_kernel<W4, EPI_I8_GELU" + (", W4R>" if _w4r() else ">"),
+        "roofline": {"bound": "mfma", "kernel": "fc1 gemm_kernel<W4, EPI_I8_GELU" + _wreg(),
                      "achieved": achieved, "peak": INT8_PEAK_TOPS, "unit": "TFLOP/s",
                      "frac": achieved / INT8_PEAK_TOPS, "traffic": traffic,
                      "ops_per_launch": ops, "launch_ms": fc1_ms,

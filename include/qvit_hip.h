@@ -72,6 +72,8 @@ extern "C" {
 #define QVIT_W8 8   /* int8 codes                                                           */
 #define QVIT_W4R 40 /* qvit_gemm / qvit_gemm_qkv_split only: QVIT_W4 codes in the register-weight image
                        (qvit_pack_weight_w4r); same results, each wave's weight rows loaded into registers */
+#define QVIT_W8R 80 /* qvit_gemm / qvit_gemm_qkv_split only: QVIT_W4 codes in the int8 register image
+                       (qvit_pack_weight_w8r); same results, no unpack in the main loop, twice the bytes  */
 #define QVIT_W16 16 /* qvit_gemm_wonly only: codes |k| <= 32639 as balanced base-256 digits k = 256 h + l, h and l
                        in [-128, 127], two QVIT_W8 images of npad * kpad bytes (h, then l; qvit_pack_weight)  */
 #define QVIT_W24 24 /* the same with three digits k = 65536 a + 256 h + l (|k| < 2^23, e.g. 16-bit layers whose
@@ -159,6 +161,17 @@ int qvit_pack_weight(const float* w, int64_t n, int64_t k, int64_t ldw, int qtyp
  * Replaces nothing in the reference: a second storage form of quantize_weight's codes (quant_layers.py:332-354).
  */
 int qvit_pack_weight_w4r(const void* packed, int64_t npad, int64_t kpad, void* out, hipStream_t stream);
+
+/*
+ * The int8 register image (QVIT_W8R) of a QVIT_W4 image from qvit_pack_weight: npad * kpad bytes (twice the W4
+ * image). In every (256-row tile, 64-deep k stage) chunk of 16 KiB the GEMM lane l of wave w finds its four 16-byte
+ * MFMA operands (rows 64 w + 16 r + (l & 15) of the tile, r = 0..3, k 16 (l >> 4) .. + 15 of the stage, each code
+ * as the byte 16 k) contiguously at byte 4096 w + 64 l. Same argument rules as qvit_pack_weight_w4r. qvit_gemm with
+ * wfmt QVIT_W8R on it gives the QVIT_W4 results byte for byte (same operands, same accumulation order) with no int4
+ * unpack in the main loop.
+ * Replaces nothing in the reference: a third storage form of quantize_weight's codes (quant_layers.py:332-354).
+ */
+int qvit_pack_weight_w8r(const void* packed, int64_t npad, int64_t kpad, void* out, hipStream_t stream);
 
 /*
  * Pads a bias vector to npad floats (zeros past n; bias may be NULL -> all zeros).

@@ -26,6 +26,7 @@ QT_FORCE_CAREFUL = 0x100  # test-only: disable the guarded fast path
 W4 = 4
 W8 = 8
 W4R = 40  # qvit_gemm / qvit_gemm_qkv_split only: a W4 image re-ordered by qvit_pack_weight_w4r
+W8R = 80  # qvit_gemm / qvit_gemm_qkv_split only: a W4 image as 16x-scaled int8 operands (qvit_pack_weight_w8r)
 W16 = 16  # qvit_gemm_wonly only: balanced base-256 digits as W8 images, two (|k| <= 32639) or
 W24 = 24  # three (|k| < 2^23)
 
@@ -61,6 +62,7 @@ _SIGNATURES = {
     "qvit_pack_weight": [_c_p, _i64, _i64, _i64, _i32, _c_p, _c_p, _c_p, _i32, _c_p, _i64, _i64, _c_p, _c_p],
     "qvit_pad_bias": [_c_p, _i64, _c_p, _i64, _c_p],
     "qvit_pack_weight_w4r": [_c_p, _i64, _i64, _c_p, _c_p],
+    "qvit_pack_weight_w8r": [_c_p, _i64, _i64, _c_p, _c_p],
     "qvit_im2col_quant_i8": [_c_p, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32,
                              _i32, _c_p, _c_p, _c_p, _i32, _c_p, _i64, _i64, _c_p],
     "qvit_layernorm_quant_i8": [_c_p, _i64, _i64, _i64, _c_p, _c_p, _f32, _i32, _c_p, _c_p, _c_p, _i32,
@@ -242,6 +244,17 @@ def pack_weight_w4r(packed: torch.Tensor, npad: int, kpad: int) -> torch.Tensor:
     out = torch.empty_like(packed)
     _check(load().qvit_pack_weight_w4r(_ptr(packed), npad, kpad, _ptr(out), _stream(packed.device)),
            "qvit_pack_weight_w4r")
+    return out
+
+
+def pack_weight_w8r(packed: torch.Tensor, npad: int, kpad: int) -> torch.Tensor:
+    """The int8 register image (wfmt W8R) of a W4 image from pack_weight (qvit_pack_weight_w8r): npad * kpad
+    bytes, each code as the byte 16 k in the GEMM lanes' operand order; qvit_gemm gives the W4 results on it."""
+    _require_gpu(packed, "packed weights")
+    assert packed.dtype == torch.uint8 and packed.is_contiguous() and packed.numel() == npad * kpad // 2
+    out = torch.empty(npad * kpad, dtype=torch.uint8, device=packed.device)
+    _check(load().qvit_pack_weight_w8r(_ptr(packed), npad, kpad, _ptr(out), _stream(packed.device)),
+           "qvit_pack_weight_w8r")
     return out
 
 

@@ -21,6 +21,9 @@ ARCH = "gfx950"
 
 SOURCES = ["quant_kernels.hip", "gemm_w4a8.hip", "gemm_ws.hip", "gemm_wonly.hip", "attention.hip",
            "qkv_attention.hip", "ultra_conv.hip"]
+# sources with inline-asm register loads: their device assembly is kept beside the objects (the very code in the
+# library) for tools/asm_load_check.py (tests/test_asm_loads.py)
+ASM_CHECKED = ["gemm_w4a8.hip", "ultra_conv.hip"]
 HEADERS = ["qvit_common.h", "attn_common.h", "attn32.h", "ln_common.h", "diag_stamps.h"]
 
 HIPCC_FLAGS = [
@@ -68,6 +71,12 @@ def is_stale(lib: str = LIB, defines: tuple = ()) -> bool:
         return True
 
 
+def device_asm(src: str, build_dir: str = BUILD, name_only: bool = False) -> str:
+    """The gfx950 device assembly hipcc -save-temps=obj kept for `src` (ASM_CHECKED)."""
+    name = f"{os.path.splitext(src)[0]}-hip-amdgcn-amd-amdhsa-{ARCH}.s"
+    return name if name_only else os.path.join(build_dir, name)
+
+
 def build(force: bool = False, verbose: bool = False, defines: tuple = (), lib: str = LIB,
           build_dir: str = BUILD) -> str:
     """Builds the library. `defines`/`lib`/`build_dir` produce diagnostic variants (e.g. the
@@ -82,6 +91,9 @@ def build(force: bool = False, verbose: bool = False, defines: tuple = (), lib: 
     def compile_one(src: str) -> str:
         obj = os.path.join(build_dir, os.path.splitext(src)[0] + ".o")
         cmd = [hipcc, *HIPCC_FLAGS, *dflags, "-I", INCLUDE, "-c", os.path.join(CSRC, src), "-o", obj]
+        keep_asm = src in ASM_CHECKED and build_dir == BUILD
+        if keep_asm:
+            cmd.insert(1, "-save-temps=obj")
         if verbose:
             print(" ".join(cmd), flush=True)
         res = subprocess.run(cmd, capture_output=True, text=True)
@@ -89,6 +101,13 @@ def build(force: bool = False, verbose: bool = False, defines: tuple = (), lib: 
             raise RuntimeError(f"hipcc failed on {src}:\n{res.stdout}\n{res.stderr}")
         if verbose and res.stderr.strip():
             print(res.stderr, file=sys.stderr)
+        if keep_asm:   # keep the device assembly, drop the other temporaries
+            stem = os.path.splitext(src)[0]
+            for f in os.listdir(build_dir):
+                if f.startswith(stem + "-") or f.startswith(stem + ".hip-"):
+                    if f == device_asm(src, build_dir, name_only=True):
+                        continue
+                    os.remove(os.path.join(build_dir, f))
         return obj
 
     with ThreadPoolExecutor(max_workers=min(4, len(SOURCES))) as ex:

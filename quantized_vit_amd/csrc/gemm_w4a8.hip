@@ -83,9 +83,23 @@ QVIT_DEV uint32_t nib16_hi(uint32_t p) { return p & 0xF0F0F0F0u; }
 // path): issued from asm, so the compiler's wait-count model never drains the asm-issued activation DMA for them;
 // the counted stage waits cover them (2 per stage and wave, as the 2 weight DMA pieces they replace)
 QVIT_DEV void ldw32(v4i& a, v4i& b, const void* sbase, uint32_t voff) {
-  asm volatile("global_load_dwordx4 %0, %2, %3\n\t"
+  asm volatile("; qvit_asm_load\n\t"
+               "global_load_dwordx4 %0, %2, %3\n\t"
                "global_load_dwordx4 %1, %2, %3 offset:16"
                : "=&v"(a), "=&v"(b)
+               : "v"(voff), "s"(sbase)
+               : "memory");
+}
+
+// The int8 register image (QVIT_W8R): a lane's four 16-B fragments of a stage, already unpacked to 16x-scaled int8
+// (16 w, exactly the operand the W4 paths unpack to), as four loads from a wave-uniform base
+QVIT_DEV void ldw64(v4i& a, v4i& b, v4i& c, v4i& d, const void* sbase, uint32_t voff) {
+  asm volatile("; qvit_asm_load\n\t"
+               "global_load_dwordx4 %0, %4, %5\n\t"
+               "global_load_dwordx4 %1, %4, %5 offset:16\n\t"
+               "global_load_dwordx4 %2, %4, %5 offset:32\n\t"
+               "global_load_dwordx4 %3, %4, %5 offset:48"
+               : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d)
                : "v"(voff), "s"(sbase)
                : "memory");
 }
@@ -104,6 +118,21 @@ __global__ void pack_w4r_kernel(const int8_t* __restrict__ src, int8_t* __restri
       *reinterpret_cast<const uint2*>(src + c * 8192 + row * 32 + ((lfq ^ (((lfr >> 3) & 1) << 1)) << 3));
 }
 
+// The int8 register image (QVIT_W8R) of a packed QVIT_W4 weight: every (tile_n, k-stage) chunk of the W4 image (8 KiB)
+// becomes 16 KiB in which wave w's 4 KiB hold lane l's four 16-B MFMA operands (rows 64 w + 16 r + (l & 15), logical
+// k-chunk l >> 4, r = 0..3, each nibble as the byte 16 w) contiguously at 64 l: the main loop loads them with four
+// coalesced 16-B loads per stage and lane and feeds them to the MFMAs with no unpack.
+__global__ void pack_w8r_kernel(const int8_t* __restrict__ src, int8_t* __restrict__ dst, int64_t nunits) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= nunits) return;
+  const int64_t c = u >> 10;
+  const int w = (int)(u >> 8) & 3, ln = (int)(u >> 2) & 63, r = (int)u & 3;
+  const int lfr = ln & 15, lfq = ln >> 4;
+  const int row = 64 * w + 16 * r + lfr;
+  const uint2 p = *reinterpret_cast<const uint2*>(src + c * 8192 + row * 32 + ((lfq ^ (((lfr >> 3) & 1) << 1)) << 3));
+  *reinterpret_cast<uint4*>(dst + c * 16384 + w * 4096 + ln * 64 + r * 16) =
+      make_uint4(nib16_lo(p.x), nib16_hi(p.x), nib16_lo(p.y), nib16_hi(p.y));
+}
 
 // Wait until at most N of this wave's DMAs are in flight, retire its LDS reads, then barrier.
 // The LDS drain is the builtin (lgkmcnt(0) = 0xC07F on gfx9) so the compiler's wait-count model sees
@@ -214,7 +243,7 @@ template <int WFMT>
 struct Frags {
   v4i x[8];
   uint2 w4[4];  // W4: packed 16 nibbles per lane
-  v4i wq[2];    // W4R: the four fragments as loaded
+  v4i wq[4];    // W4R: the four fragments as loaded (wq[0..1]); W8R: the four int8 operands
   v4i w8[4];    // W8: 16 bytes per lane
 };
 
@@ -241,10 +270,16 @@ QVIT_DEV void st_resid(float* dst, float4 o, const float* C0, int M, int64_t ldc
 // The operand stages form one stream across the block's tiles: the last two steps of a tile issue the
 // DMA of the next tile's first two stages, so the pipeline never drains between tiles.
 //
-// RW (QVIT_W4R weights): each wave's 64 weight rows are its own, so they come straight into registers (two 16-B
-// loads per stage and lane, one stage ahead of their MFMAs) instead of through an LDS-DMA piece and a fragment
-// read; the activations stay on the LDS-DMA ring (round 5: fc1 -2.6 % in the model, same box).
-template <int WFMT, int EPI, int WM, bool RW>
+// RW (register weights): each wave's 64 weight rows are its own, so they come straight into registers, one stage
+// ahead of their MFMAs, instead of through an LDS-DMA piece and a fragment read; the activations stay on the LDS-DMA
+// ring. RW 1 = QVIT_W4R (two 16-B loads per stage and lane, unpacked like the LDS form; round 5: fc1 -2.6 % in the
+// model, same box), RW 2 = QVIT_W8R (the same operands already unpacked: four 16-B loads, no unpack VALU).
+//
+// L2 (register weights, K >= 256): the activation stream runs two stages ahead instead of one, through a 4-slot ring
+// of activation-only slots (8 KiB; the weight half of a slot is unused with register weights): step kt issues stage
+// kt + 3's pieces and waits for stage kt + 1's, so a stage has two steps to land instead of one. The same barriers,
+// reads and MFMAs per step; LDS 32 KiB of ring instead of 48.
+template <int WFMT, int EPI, int WM, int RW, bool L2 = false>
 __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) void gemm_kernel(
     const int8_t* __restrict__ A, int M, int K, int64_t lda, const int8_t* __restrict__ Wp, int N, int npad,
     void* __restrict__ C, int64_t ldc, EpiArgs ep) {
@@ -252,13 +287,19 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   constexpr int BM = G::BM;
   constexpr int XBYTES = G::XBYTES;
   constexpr bool I8OUT = (EPI == QVIT_EPI_I8 || EPI == QVIT_EPI_I8_GELU);
-  __shared__ __attribute__((aligned(16))) int8_t smem[G::LDS];
-  int8_t* epi_lds = smem + G::RING_BYTES;
-  const float* bias_l = reinterpret_cast<const float*>(smem + G::RING_BYTES + G::EPI_BYTES);
-  QParams* qp_l = reinterpret_cast<QParams*>(smem + G::RING_BYTES + G::EPI_BYTES + G::BIAS_BYTES);
+  static_assert(!L2 || RW != 0, "the two-ahead activation ring is for register weights");
+  constexpr int RINGN = L2 ? 4 : RING;                    // ring slots
+  constexpr int SLOT = L2 ? XBYTES : G::STAGE;            // bytes per slot
+  constexpr int RING_B = RINGN * SLOT;
+  __shared__ __attribute__((aligned(16))) int8_t smem[RING_B + G::EPI_BYTES + G::BIAS_BYTES + G::QP_BYTES];
+  int8_t* epi_lds = smem + RING_B;
+  const float* bias_l = reinterpret_cast<const float*>(smem + RING_B + G::EPI_BYTES);
+  QParams* qp_l = reinterpret_cast<QParams*>(smem + RING_B + G::EPI_BYTES + G::BIAS_BYTES);
   const bool has_bias = (EPI != QVIT_EPI_I32) && ep.bias != nullptr;
-  constexpr bool REGW = RW;
+  constexpr bool REGW = RW != 0;
   static_assert(!RW || (WFMT == QVIT_W4 && WM == 1), "register weights: the W4 4-wave tile");
+  constexpr int WREG = RW == 2 ? 4 : 2;                        // register loads per stage and wave (REGW)
+  constexpr int WIMG = RW == 2 ? 2 * G::WBYTES : G::WBYTES;   // weight image bytes per (tile_n, stage)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -308,50 +349,48 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   constexpr int WROWS_PER_PIECE = 1024 / G::WROW;
   constexpr int WROWS_PER_WAVE = BN / G::NWAVES;
   const int nk = K / BK;  // even, >= 2
-  // a tile's sources are uniform (m0, weight-tile base); the per-lane parts are tile-invariant
-  // byte offsets from the A / Wp kernel arguments fit 32 bits (checked by the launcher)
-  // LEAN (the fp32 / int32 epilogues): the per-lane parts of a tile's DMA sources (activation rows, clamped at
-  // the tail; the weight pieces' lane offset) and of its fragment reads are computed once per tile at its head,
-  // from an opaque lane id so that none of them stays live across the epilogue; a stage only moves the uniform
-  // SGPR bases (round 5: fc2 -2 %, measured). The int8-code epilogues need every register of the budget (their
-  // table lookups), so there the offsets are recomputed from the lane id at each use, as before (the lean form
-  // spilled).
-  constexpr bool LEAN = !I8OUT;
-  // per tile: the weight tile's byte offset in Wp (uniform) and the per-lane byte offsets from A of the tile's
-  // stage-0 activation pieces
+  // The per-lane parts of the DMA sources are tile-invariant: piece j of wave w stages the tile's rows
+  // 32 w + 16 j + (lane >> 2), 16-B chunk (lane & 3) swizzled by row bit 2 (= lane bit 4, as 32 w + 16 j has no bit
+  // below 4), so the lane offset (lane >> 2) lda + chunk is one value for every piece, wave and whole tile; the row
+  // base m0 + 32 w + 16 j and the stage's k offset ride in the SGPR base (a 64-bit scalar add per piece, no VALU).
+  // Only a tail tile (rows past M, clamped to M - 1 so no read leaves A) computes per-lane row offsets. The lane
+  // offsets (DMA sources, fragment reads, weight slices) are computed at each tile head from an opaque lane id, so
+  // none of them is live across the epilogue (the int8-code epilogues need every register of the budget) and a
+  // stage does no per-lane address arithmetic.
+  // PEEL (the fp32 / int32 epilogues on the W4 images): the tile's first stage accumulates onto zero (peeled)
+  // instead of clearing the accumulators (the peeled copy of the step does not fit the W8R registers).
+  constexpr bool PEEL = !I8OUT && RW != 2;
   uint32_t wlane = 0;
   auto tile_w = [&](int tt) -> uint32_t {
-    return __builtin_amdgcn_readfirstlane((uint32_t)(tt % nb_n) * (uint32_t)(nk * G::WBYTES));
+    return __builtin_amdgcn_readfirstlane((uint32_t)(tt % nb_n) * (uint32_t)(nk * WIMG));
   };
-  auto tile_a = [&](int tt, uint32_t (&a)[G::XPIECES], int ln) __attribute__((always_inline)) {
-    const int m0 = (tt / nb_n) * BM;
-#pragma unroll
-    for (int j = 0; j < G::XPIECES; ++j) {
-      const int row = 32 * wave + 16 * j + (ln >> 2);
-      int gm = m0 + row;
-      gm = gm < M ? gm : M - 1;  // clamp the tail: staged, never stored
-      a[j] = (uint32_t)gm * (uint32_t)lda + (uint32_t)(((ln & 3) ^ (((row >> 2) & 1) << 1)) * 16);
-    }
+  auto tile_m0 = [&](int tt) -> int { return __builtin_amdgcn_readfirstlane((tt / nb_n) * BM); };
+  auto lane_a = [&](int ln) -> uint32_t {
+    return (uint32_t)(ln >> 2) * (uint32_t)lda + (uint32_t)(((ln & 3) ^ (((ln >> 4) & 1) << 1)) << 4);
   };
+  uint32_t alane = 0;
   const uint32_t lds0 = lds_addr(smem);
-  auto issue = [&](int tt, uint32_t wt, const uint32_t (&a_in)[G::XPIECES], int kt, int rslot) __attribute__((always_inline)) {
-    const uint32_t sx = lds0 + (uint32_t)(rslot * G::STAGE);
+  auto issue = [&](int m0, uint32_t wt, int kt, int rslot) __attribute__((always_inline)) {
+    const uint32_t sx = lds0 + (uint32_t)(rslot * SLOT);
     const uint32_t sw = sx + XBYTES;
-    const int8_t* abase = A + kt * BK;
-    uint32_t a[G::XPIECES];
-    uint32_t wl = wlane;
-    if constexpr (LEAN) {
+    if (m0 + BM <= M) {
+      const int8_t* abase = A + (int64_t)(m0 + 32 * wave) * lda + kt * BK;
 #pragma unroll
-      for (int j = 0; j < G::XPIECES; ++j) a[j] = a_in[j];
+      for (int j = 0; j < G::XPIECES; ++j)
+        dma16s(abase + (int64_t)(16 * j) * lda, alane, __builtin_amdgcn_readfirstlane(sx + (32 * wave + 16 * j) * BK));
     } else {
       const int ln = lane_opaque();
-      tile_a(tt, a, ln);
-      wl = (uint32_t)ln * 16u;
-    }
 #pragma unroll
-    for (int j = 0; j < G::XPIECES; ++j)
-      dma16s(abase, a[j], __builtin_amdgcn_readfirstlane(sx + (32 * wave + 16 * j) * BK));
+      for (int j = 0; j < G::XPIECES; ++j) {
+        const int row = 32 * wave + 16 * j + (ln >> 2);
+        int gm = m0 + row;
+        gm = gm < M ? gm : M - 1;  // clamp the tail: staged, never stored
+        const uint32_t a = (uint32_t)gm * (uint32_t)lda + (uint32_t)(((ln & 3) ^ (((row >> 2) & 1) << 1)) * 16);
+        dma16s(A + kt * BK, a, __builtin_amdgcn_readfirstlane(sx + (32 * wave + 16 * j) * BK));
+      }
+    }
     if constexpr (!REGW) {
+      const uint32_t wl = wlane;
       const int8_t* wbase = Wp + wt + (uint32_t)kt * G::WBYTES + (uint32_t)(wave * (G::WPIECES * 1024));
       // (piece j's 1-KiB step rides in the SGPR base: an instruction offset would move the LDS address too)
 #pragma unroll
@@ -362,16 +401,20 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   // REGW: this wave's weight slice of stage kt -> f.wq (issued one stage ahead of its MFMAs: the stage wait of the
   // next step, which counts 4 younger operations, covers it)
   auto issue_w = [&](uint32_t wt, int kt, Frags<WFMT>& f) __attribute__((always_inline)) {
-    if constexpr (REGW) {
-      const int8_t* wbase = Wp + wt + (uint32_t)kt * G::WBYTES + (uint32_t)(wave * (G::WPIECES * 1024));
-      ldw32(f.wq[0], f.wq[1], wbase, (uint32_t)lane_opaque() * 32u);
+    if constexpr (RW == 1) {
+      const int8_t* wbase = Wp + wt + (uint32_t)kt * WIMG + (uint32_t)(wave * (WIMG / 4));
+      ldw32(f.wq[0], f.wq[1], wbase, wlane * 2u);
+    } else if constexpr (RW == 2) {
+      const int8_t* wbase = Wp + wt + (uint32_t)kt * WIMG + (uint32_t)(wave * (WIMG / 4));
+      ldw64(f.wq[0], f.wq[1], f.wq[2], f.wq[3], wbase, wlane * 4u);
     }
   };
   // the loads of f.wq have landed (a counted wait above): tied here, so no use of them is scheduled earlier
   auto pin = [&](Frags<WFMT>& f) __attribute__((always_inline)) {
-    if constexpr (REGW) asm volatile("" : "+v"(f.wq[0]), "+v"(f.wq[1]));
+    if constexpr (RW == 1) asm volatile("; qvit_pin %0 %1" : "+v"(f.wq[0]), "+v"(f.wq[1]));
+    if constexpr (RW == 2)
+      asm volatile("; qvit_pin %0 %1 %2 %3" : "+v"(f.wq[0]), "+v"(f.wq[1]), "+v"(f.wq[2]), "+v"(f.wq[3]));
   };
-
   // per-lane fragment offsets inside a stage (set at each tile head; one add per stage moves them to the slot)
   int xoff = 0, woff = 0;
   auto lane_offsets = [&](int ln) __attribute__((always_inline)) {
@@ -380,10 +423,10 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     woff = (WFMT == QVIT_W4) ? (64 * wn + lfr) * G::WROW + ((lfq ^ (((lfr >> 3) & 1) << 1)) << 3)
                              : (64 * wn + lfr) * G::WROW + ((lfq ^ (((lfr >> 2) & 1) << 1)) << 4);
     wlane = (uint32_t)ln * 16u;
+    alane = lane_a(ln);
   };
   auto read_frags = [&](int rslot, Frags<WFMT>& f) {
-    if constexpr (!LEAN) lane_offsets(lane_opaque());
-    const int8_t* sx = smem + rslot * G::STAGE;
+    const int8_t* sx = smem + rslot * SLOT;
     const int8_t* sw = sx + XBYTES;
 #pragma unroll
     for (int s = 0; s < 8; ++s) f.x[s] = *reinterpret_cast<const v4i*>(sx + xoff + s * 16 * BK);
@@ -405,7 +448,9 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       v4i wf;
-      if (WFMT == QVIT_W4) {
+      if constexpr (RW == 2) {
+        wf = f.wq[r];
+      } else if (WFMT == QVIT_W4) {
         uint2 p = f.w4[r];
         if constexpr (REGW) {
           const v4i q = f.wq[r >> 1];
@@ -424,7 +469,8 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   // One pipeline step: stage kt is in registers (cur); bring stage kt+1 into registers (nxt).
   // The phases are fenced (sched_barrier) and the LDS drain at the top is compiler-visible, so the
   // fragment reads of stage kt+1 overlap the MFMAs of stage kt with no wait between them.
-  constexpr int D = G::DMA_PER_STAGE;
+  // memory operations per stage and wave: the activation pieces + the weight pieces (LDS) or register loads
+  constexpr int D = G::XPIECES + (REGW ? WREG : G::WPIECES);
   auto step_core = [&](Frags<WFMT>& cur, Frags<WFMT>& nxt, int next_slot, bool read,
                        auto zeroc) __attribute__((always_inline)) {
     if (read) read_frags(next_slot, nxt);
@@ -540,14 +586,14 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
 
   // prologue: the first tile's stages 0 and 1 (the Src values are scoped to one tile: nothing of them is
   // carried across a loop iteration)
-  int g = 0;  // global stage counter of this block (ring slot = g % RING)
+  int g = 0;  // global stage counter of this block (ring slot = g % RINGN)
   {
-    uint32_t a0[G::XPIECES];
     lane_offsets(lane_opaque());
-    tile_a(t, a0, lane_opaque());
+    const int am0 = tile_m0(t);
     const uint32_t w0 = tile_w(t);
-    issue(t, w0, a0, 0, 0);
-    issue(t, w0, a0, 1, 1);
+    issue(am0, w0, 0, 0);
+    issue(am0, w0, 1, 1);
+    if constexpr (L2) issue(am0, w0, 2, 2);
   }
   Frags<WFMT> fa, fb;
   QVIT_STAMP_DECL
@@ -555,39 +601,131 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   for (;;) {
     const int tnext = t + team;
     const bool has_next = tnext < hi;
-    const int m0 = (t / nb_n) * BM, n0 = (t % nb_n) * BN;
-    if (nk == 2 || !LEAN) {  // (K = 128: no steady step, the tail's first stage is the tile's first)
+    const int m0 = tile_m0(t), n0 = (t % nb_n) * BN;
+    if (nk == 2 || !PEEL) {  // (K = 128: no steady step, the tail's first stage is the tile's first)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int s = 0; s < 8; ++s) acc[r][s] = v4i{0, 0, 0, 0};
     }
 
+    if constexpr (L2) {
+    // Two-ahead activation stream. Memory operations in issue order (XP = G::XPIECES, WREG per stage and wave):
+    // step kt issues w(kt + 1) then act(kt + 3), so the wait of step kt, which needs act(kt + 1) and w(kt), leaves
+    // exactly act(kt + 2), w(kt + 1), act(kt + 3) in flight: vmcnt(2 XP + WREG). The tail steps nk-3 .. nk-1 issue
+    // the next tile's stages 0 .. 2 in the place of act(kt + 3) (or nothing: the counts shrink by XP each).
+    // Ring slot safety: act(kt + 3) lands in the slot of stage kt - 1, whose fragments every wave read in step
+    // kt - 2, before the barrier of step kt - 1.
+    constexpr int DS = 2 * G::XPIECES + WREG;
+    QVIT_STAMP(5);
+    const uint32_t cw = tile_w(t);
+    const int ln = lane_opaque();
+    lane_offsets(ln);
+    issue_w(cw, 0, fa);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    stage_sync<DS>();  // act(0): at most act(1), act(2), w(0) are younger and still in flight
+    QVIT_STAMP(0);
+    QVIT_LSTAMP(0);
+    if (has_bias && wave == 0)
+      dma16(ep.bias + n0 + ln * 4, __builtin_amdgcn_readfirstlane(lds0 + RING_B + G::EPI_BYTES));
+    read_frags(g % RINGN, fa);
+    // step 0 (accumulators start at zero when PEEL): needs act(1), w(0); younger: w(1), act(3)
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_sched_barrier(0);
+    issue_w(cw, 1, fb);
+    issue(m0, cw, 3, (g + 3) % RINGN);
+    QVIT_STAMP(1);
+    stage_sync<G::XPIECES + WREG>();
+    pin(fa);
+    QVIT_STAMP(2);
+    if constexpr (PEEL) step_core(fa, fb, (g + 1) % RINGN, true, std::true_type{});
+    else step_core(fa, fb, (g + 1) % RINGN, true, std::false_type{});
+    QVIT_STAMP(3);
+    // steady steps 1 .. nk-4 in pairs (stage kt in fb, then kt + 1 in fa)
+    for (int kt = 1; kt + 1 <= nk - 4; kt += 2) {
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_sched_barrier(0);
+      issue_w(cw, kt + 1, fa);
+      issue(m0, cw, kt + 3, (g + kt + 3) % RINGN);
+      QVIT_STAMP(1);
+      stage_sync<DS>();
+      pin(fb);
+      QVIT_STAMP(2);
+      step_core(fb, fa, (g + kt + 1) % RINGN, true, std::false_type{});
+      QVIT_STAMP(3);
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_sched_barrier(0);
+      issue_w(cw, kt + 2, fb);
+      issue(m0, cw, kt + 4, (g + kt + 4) % RINGN);
+      QVIT_STAMP(1);
+      stage_sync<DS>();
+      pin(fa);
+      QVIT_STAMP(2);
+      step_core(fa, fb, (g + kt + 2) % RINGN, true, std::false_type{});
+      QVIT_STAMP(3);
+    }
+    // tail steps nk-3, nk-2, nk-1: the next tile's stages 0, 1, 2 (the weight loads go out before the branches,
+    // so every path from a load to its use holds a covering wait: tools/asm_load_check.py)
+    const uint32_t nw = has_next ? tile_w(tnext) : 0u;
+    const int nm0 = has_next ? tile_m0(tnext) : 0;
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_sched_barrier(0);
+    issue_w(cw, nk - 2, fa);
+    if (has_next) {
+      issue(nm0, nw, 0, (g + nk) % RINGN);
+      stage_sync<DS>();
+    } else {
+      stage_sync<G::XPIECES + WREG>();
+    }
+    pin(fb);
+    step_core(fb, fa, (g + nk - 2) % RINGN, true, std::false_type{});
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_sched_barrier(0);
+    issue_w(cw, nk - 1, fb);
+    if (has_next) {
+      issue(nm0, nw, 1, (g + nk + 1) % RINGN);
+      stage_sync<DS>();
+    } else {
+      stage_sync<WREG>();
+    }
+    pin(fa);
+    step_core(fa, fb, (g + nk - 1) % RINGN, true, std::false_type{});
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_sched_barrier(0);
+    if (has_next) {
+      issue(nm0, nw, 2, (g + nk + 2) % RINGN);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G::XPIECES) : "memory");  // w(nk - 1); younger: next 1, 2
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    pin(fb);
+    step_core(fb, fa, 0, false, std::false_type{});
+    QVIT_STAMP(3);
+    QVIT_LSTAMP(1);
+    } else {
     // head: stage 0 of this tile landed (stage 1 may still be in flight); every wave is past the
     // previous tile's epilogue, so the tile's bias can be DMA'd into its LDS slot (1 KiB, wave 0;
     // older than every later stage DMA, so the counted stage waits cover it)
     QVIT_STAMP(5);
     const uint32_t cw = tile_w(t);
+    const int ln = lane_opaque();
+    lane_offsets(ln);
     issue_w(cw, 0, fa);  // REGW: stage 0's weights (covered by the first stage wait below the head)
     __builtin_amdgcn_s_waitcnt(0xC07F);
     stage_sync<D>();
     QVIT_STAMP(0);
     QVIT_LSTAMP(0);
-    uint32_t ca[G::XPIECES];
     {
-      const int ln = lane_opaque();
-      lane_offsets(ln);
-      tile_a(t, ca, ln);
       if (has_bias && wave == 0)
-        dma16(ep.bias + n0 + ln * 4, __builtin_amdgcn_readfirstlane(lds0 + G::RING_BYTES + G::EPI_BYTES));
+        dma16(ep.bias + n0 + ln * 4, __builtin_amdgcn_readfirstlane(lds0 + RING_B + G::EPI_BYTES));
     }
-    read_frags(g % RING, fa);
+    read_frags(g % RINGN, fa);
     // steady steps kt = 0 .. nk-3: issue this tile's stage kt+2 (the first one peeled: zero accumulators)
     int kt = 0;
-    if (LEAN && nk > 2) {
+    if (PEEL && nk > 2) {
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_sched_barrier(0);
-      issue(t, cw, ca, 2, (g + 2) % RING);
+      issue(m0, cw, 2, (g + 2) % RINGN);
       issue_w(cw, 1, fb);
       QVIT_STAMP(1);
       stage_sync<D>();
@@ -597,7 +735,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
       QVIT_STAMP(3);
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_sched_barrier(0);
-      issue(t, cw, ca, 3, (g + 3) % RING);
+      issue(m0, cw, 3, (g + 3) % RINGN);
       issue_w(cw, 2, fa);
       QVIT_STAMP(1);
       stage_sync<D>();
@@ -610,7 +748,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     for (; kt < nk - 2; kt += 2) {
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_sched_barrier(0);
-      issue(t, cw, ca, kt + 2, (g + kt + 2) % RING);
+      issue(m0, cw, kt + 2, (g + kt + 2) % RINGN);
       issue_w(cw, kt + 1, fb);
       QVIT_STAMP(1);
       stage_sync<D>();
@@ -620,7 +758,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
       QVIT_STAMP(3);
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_sched_barrier(0);
-      issue(t, cw, ca, kt + 3, (g + kt + 3) % RING);
+      issue(m0, cw, kt + 3, (g + kt + 3) % RINGN);
       issue_w(cw, kt + 2, fa);
       QVIT_STAMP(1);
       stage_sync<D>();
@@ -632,32 +770,35 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     // tail kt = nk-2, nk-1: issue the next tile's stages 0, 1
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_sched_barrier(0);
-    uint32_t na[G::XPIECES];
     const uint32_t nw = has_next ? tile_w(tnext) : 0u;
+    const int nm0 = has_next ? tile_m0(tnext) : 0;
+    // (REGW: the last stage's weights go out before the branches, so every path from their load to their pin
+    // holds a covering wait - tools/asm_load_check.py walks all of them - and the counts are those of the steady
+    // steps: with a next tile, stage_sync<D> leaves exactly the weights and the next tile's stage-0 pieces in flight)
+    issue_w(cw, nk - 1, fb);
     if (has_next) {
-      tile_a(tnext, na, lane_opaque());  // (here, not at the tile head: this tile's offsets are dead by now)
-      issue(tnext, nw, na, 0, (g + nk) % RING);
-      issue_w(cw, nk - 1, fb);
+      issue(nm0, nw, 0, (g + nk) % RINGN);
       stage_sync<D>();
-    } else if constexpr (REGW) {
-      issue_w(cw, nk - 1, fb);
-      stage_sync<2>();
     } else {
-      stage_sync<0>();
+      stage_sync<REGW ? WREG : 0>();
     }
     pin(fa);
     step_core(fa, fb, (g + nk - 1) % RING, true, std::false_type{});
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_sched_barrier(0);
-    if (has_next) issue(tnext, nw, na, 1, (g + nk + 1) % RING);
-    if constexpr (REGW) {  // the last stage's weights (younger: the next tile's stage-1 pieces, if any)
-      if (has_next) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      pin(fb);
+    if (has_next) {
+      issue(nm0, nw, 1, (g + nk + 1) % RINGN);
+      // the last stage's weights (younger: the next tile's stage-1 pieces)
+      if constexpr (REGW) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::XPIECES) : "memory");
+    } else {
+      if constexpr (REGW) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    pin(fb);
     step_core(fb, fa, 0, false, std::false_type{});
     QVIT_STAMP(3);
     QVIT_LSTAMP(1);
+
+    }
 
     if (WFMT == QVIT_W4 && EPI == QVIT_EPI_I32) {  // 16 acc -> acc (exact arithmetic shift)
 #pragma unroll
@@ -752,7 +893,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const float* src = Cf + (int64_t)(m0 + 128 * wm + 16 * sr + 4 * i + prow) * ldc + n;
-            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(ov[i]) : "v"(src) : "memory");
+            asm volatile("; qvit_asm_load\n\tglobal_load_dwordx4 %0, %1, off" : "=v"(ov[i]) : "v"(src) : "memory");
           }
         };
         auto pass = [&](int sr, f4v (&ov)[4]) __attribute__((always_inline)) {
@@ -764,9 +905,11 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
           __builtin_amdgcn_wave_barrier();
           // tie the wait to the loaded registers, so no use of them is scheduled above it
           if (sr == 0 || sr == 7)
-            asm volatile("s_waitcnt vmcnt(4)" : "+v"(ov[0]), "+v"(ov[1]), "+v"(ov[2]), "+v"(ov[3]) :: "memory");
+            asm volatile("s_waitcnt vmcnt(4)\n\t; qvit_pin %0 %1 %2 %3"
+                         : "+v"(ov[0]), "+v"(ov[1]), "+v"(ov[2]), "+v"(ov[3]) :: "memory");
           else
-            asm volatile("s_waitcnt vmcnt(8)" : "+v"(ov[0]), "+v"(ov[1]), "+v"(ov[2]), "+v"(ov[3]) :: "memory");
+            asm volatile("s_waitcnt vmcnt(8)\n\t; qvit_pin %0 %1 %2 %3"
+                         : "+v"(ov[0]), "+v"(ov[1]), "+v"(ov[2]), "+v"(ov[3]) :: "memory");
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int row = 4 * i + prow;
@@ -979,7 +1122,12 @@ int device_cus() {
   return cus;
 }
 
-template <int WFMT, int EPI, bool RW = false>
+#ifndef QVIT_GEMM_L2
+#define QVIT_GEMM_L2 1
+#endif
+constexpr bool GEMM_L2 = QVIT_GEMM_L2 != 0;  // (diagnostic builds: -DQVIT_GEMM_L2=0 for the one-ahead ring)
+
+template <int WFMT, int EPI, int RW = 0>
 int launch(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int64_t N, int64_t npad,
            void* C, int64_t ldc, const EpiArgs& ep, hipStream_t stream) {
   constexpr int WMV = 1;   // (a second W4 tile width was measured slower in round 3: DESIGN.md section 8)
@@ -988,7 +1136,7 @@ int launch(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, i
   // chunks whose A span stays below 2^32 (one chunk for every ViT / UltraNet shape)
   const int64_t span = (int64_t)0xFFFFFFFF - K;
   int64_t rows = span / lda / G::BM * G::BM;
-  if (rows < G::BM || npad * (K / (WFMT == QVIT_W4 ? 2 : 1)) > span) return QVIT_EINVAL;
+  if (rows < G::BM || npad * (K / (WFMT == QVIT_W4 && RW != 2 ? 2 : 1)) > span) return QVIT_EINVAL;
   if (EPI == QVIT_EPI_QKV_SPLIT && rows < M) return QVIT_EINVAL;  // its row -> (image, token) map is global
   const int64_t esize = (EPI == QVIT_EPI_I8 || EPI == QVIT_EPI_I8_GELU) ? 1 : 4;
   for (int64_t m0 = 0; m0 < M; m0 += rows) {
@@ -1005,15 +1153,22 @@ int launch(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, i
       epc.ln_cnt = ep.ln_cnt + m0 / G::BM;
       epc.ln_codes = ep.ln_codes + m0 * ep.ln_ldc;
     }
-    hipLaunchKernelGGL((gemm_kernel<WFMT, EPI, WMV, RW>), dim3((unsigned)grid), dim3(G::NT), 0, stream, A + m0 * lda,
-                       (int)mc, (int)K, lda, reinterpret_cast<const int8_t*>(Wp), (int)N, (int)npad, Cc, ldc, epc);
+    // register weights and K >= 256 (4 stages or more per tile): the two-ahead activation ring
+    if (RW != 0 && K >= 256 && GEMM_L2)
+      hipLaunchKernelGGL((gemm_kernel<WFMT, EPI, WMV, RW, RW != 0>), dim3((unsigned)grid), dim3(G::NT), 0, stream,
+                         A + m0 * lda, (int)mc, (int)K, lda, reinterpret_cast<const int8_t*>(Wp), (int)N, (int)npad, Cc,
+                         ldc, epc);
+    else
+      hipLaunchKernelGGL((gemm_kernel<WFMT, EPI, WMV, RW>), dim3((unsigned)grid), dim3(G::NT), 0, stream,
+                         A + m0 * lda, (int)mc, (int)K, lda, reinterpret_cast<const int8_t*>(Wp), (int)N, (int)npad, Cc,
+                         ldc, epc);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return qvit_hip_status(e);
   }
   return QVIT_OK;
 }
 
-template <int WFMT, bool RW = false>
+template <int WFMT, int RW = 0>
 int dispatch_epi(int epilogue, const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int64_t N,
                  int64_t npad, void* C, int64_t ldc, const EpiArgs& ep, hipStream_t stream) {
   switch (epilogue) {
@@ -1062,12 +1217,23 @@ extern "C" int qvit_pack_weight_w4r(const void* packed, int64_t npad, int64_t kp
   return qvit_hip_status(hipGetLastError());
 }
 
+extern "C" int qvit_pack_weight_w8r(const void* packed, int64_t npad, int64_t kpad, void* out, hipStream_t stream) {
+  if (!packed || !out) return QVIT_ENULL;
+  if (npad <= 0 || npad % BN || kpad <= 0 || kpad % KTILE || npad > INT32_MAX / 2 || kpad > 65536) return QVIT_EINVAL;
+  if ((((uintptr_t)packed) & 15) || (((uintptr_t)out) & 15)) return QVIT_EALIGN;
+  if (packed == out) return QVIT_EINVAL;  // not in place
+  const int64_t units = npad * kpad / 16;  // 8-B source slices -> 16-B operands (npad kpad bytes out)
+  hipLaunchKernelGGL(pack_w8r_kernel, dim3((unsigned)((units + 255) / 256)), dim3(256), 0, stream,
+                     reinterpret_cast<const int8_t*>(packed), reinterpret_cast<int8_t*>(out), units);
+  return qvit_hip_status(hipGetLastError());
+}
+
 extern "C" int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, int wfmt, int64_t N,
                          int64_t npad, const float* d_act, const float* d_wt, const float* bias, int epilogue,
                          void* C, int64_t ldc, int out_qtype, const float* out_d, const float* out_qm,
                          const float* out_t, int out_levels, const void* epi_table, hipStream_t stream) {
   if (!A || !Wp || !C) return QVIT_ENULL;
-  if (wfmt != QVIT_W4 && wfmt != QVIT_W4R && wfmt != QVIT_W8) return QVIT_EINVAL;
+  if (wfmt != QVIT_W4 && wfmt != QVIT_W4R && wfmt != QVIT_W8R && wfmt != QVIT_W8) return QVIT_EINVAL;
   if (M < 0 || K <= 0 || K % KTILE || lda < K || N <= 0 || npad < N || npad % BN) return QVIT_EINVAL;
   if (M > INT32_MAX / 2 || npad > INT32_MAX / 2 || K > (1 << 24)) return QVIT_EINVAL;
   if (wfmt != QVIT_W8 && K > 65536) return QVIT_EINVAL;  // 16x-scaled int32 accumulation bound
@@ -1090,7 +1256,8 @@ extern "C" int qvit_gemm(const int8_t* A, int64_t M, int64_t K, int64_t lda, con
   EpiArgs ep{d_act, d_wt, bias, out_qtype, out_d, out_qm, out_t, out_levels,
              (i8out ? reinterpret_cast<const int8_t*>(epi_table) : nullptr), 1, 1.f, 1.f, nullptr};
   if (wfmt == QVIT_W4) return dispatch_epi<QVIT_W4>(epilogue, A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
-  if (wfmt == QVIT_W4R) return dispatch_epi<QVIT_W4, true>(epilogue, A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
+  if (wfmt == QVIT_W4R) return dispatch_epi<QVIT_W4, 1>(epilogue, A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
+  if (wfmt == QVIT_W8R) return dispatch_epi<QVIT_W4, 2>(epilogue, A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
   return dispatch_epi<QVIT_W8>(epilogue, A, M, K, lda, Wp, N, npad, C, ldc, ep, stream);
 }
 
@@ -1131,7 +1298,7 @@ extern "C" int qvit_gemm_qkv_split(const int8_t* A, int64_t M, int64_t K, int64_
                                    int64_t N, int64_t npad, const float* d_act, const float* d_wt, const float* bias,
                                    int64_t seq, float in_scale, void* qkv_hi, void* qkv_lo, hipStream_t stream) {
   if (!A || !Wp || !qkv_hi || !qkv_lo || !d_act || !d_wt) return QVIT_ENULL;
-  if (wfmt != QVIT_W4 && wfmt != QVIT_W4R && wfmt != QVIT_W8) return QVIT_EINVAL;
+  if (wfmt != QVIT_W4 && wfmt != QVIT_W4R && wfmt != QVIT_W8R && wfmt != QVIT_W8) return QVIT_EINVAL;
   if (M < 0 || K <= 0 || K % KTILE || lda < K || N <= 0 || N % 64 || npad < N || npad % BN) return QVIT_EINVAL;
   if (M > INT32_MAX / 2 || npad > INT32_MAX / 2 || K > (1 << 24)) return QVIT_EINVAL;
   if (seq <= 0 || seq > (1 << 20) || M % seq || !(in_scale > 0.f)) return QVIT_EINVAL;
@@ -1145,6 +1312,8 @@ extern "C" int qvit_gemm_qkv_split(const int8_t* A, int64_t M, int64_t K, int64_
   if (wfmt == QVIT_W4)
     return launch<QVIT_W4, QVIT_EPI_QKV_SPLIT>(A, M, K, lda, Wp, N, npad, qkv_hi, N, ep, stream);
   if (wfmt == QVIT_W4R)
-    return launch<QVIT_W4, QVIT_EPI_QKV_SPLIT, true>(A, M, K, lda, Wp, N, npad, qkv_hi, N, ep, stream);
+    return launch<QVIT_W4, QVIT_EPI_QKV_SPLIT, 1>(A, M, K, lda, Wp, N, npad, qkv_hi, N, ep, stream);
+  if (wfmt == QVIT_W8R)
+    return launch<QVIT_W4, QVIT_EPI_QKV_SPLIT, 2>(A, M, K, lda, Wp, N, npad, qkv_hi, N, ep, stream);
   return launch<QVIT_W8, QVIT_EPI_QKV_SPLIT>(A, M, K, lda, Wp, N, npad, qkv_hi, N, ep, stream);
 }

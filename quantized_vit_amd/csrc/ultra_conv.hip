@@ -856,23 +856,28 @@ __global__ __launch_bounds__(512, 1) void ultra_tail_kernel(const int8_t* __rest
   // (64 x 576 B = 4.5 16-B pieces per thread), and written to LDS once every wave is done with the current ones
   constexpr int WPT = (64 * 36 + 511) / 512;
   v4i wpre[WPT];
-  auto fetch_w = [&](const int8_t* w, int rows, int kbytes, int kp) __attribute__((always_inline)) {
-    const int per = kbytes / 16;
+  // head: the 1x1 head's 48 x 64-B rows instead of a 3x3 layer's 64 x 576-B rows. Each load and its wait (put_w) have
+  // one call site in the layer loop, selected by `head` rather than by two branches: with two sites the compiler
+  // gave the prefetch registers two homes and copied one into the other before the wait, i.e. before the data had
+  // landed (found by tools/asm_load_check.py)
+  auto fetch_w = [&](const int8_t* w, bool head, int kp) __attribute__((always_inline)) {
+    const int per = head ? 4 : 36, rows = head ? 48 : 64;
 #pragma unroll
     for (int k = 0; k < WPT; ++k) {
-      const int i = tid + 512 * k, o = i / per, c16 = i - o * per;
+      const int i = tid + 512 * k, o = head ? i >> 2 : i / 36, c16 = i - o * per;
       // (issued from asm: the compiler would drain an ordinary load before the patch loop that it outlives)
       const int8_t* src = w + (int64_t)(i < rows * per ? o : 0) * kp + 16 * (i < rows * per ? c16 : 0);
-      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(wpre[k]) : "v"(src) : "memory");
+      asm volatile("; qvit_asm_load\n\tglobal_load_dwordx4 %0, %1, off" : "=v"(wpre[k]) : "v"(src) : "memory");
     }
   };
-  auto put_w = [&](int rows, int kbytes, int stride) __attribute__((always_inline)) {
-    const int per = kbytes / 16;
+  auto put_w = [&](bool head) __attribute__((always_inline)) {
+    const int per = head ? 4 : 36, rows = head ? 48 : 64, stride = head ? TL_HSTR : TL_WSTR;
     static_assert(WPT == 5, "the wait's operand list");
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(wpre[0]), "+v"(wpre[1]), "+v"(wpre[2]), "+v"(wpre[3]), "+v"(wpre[4])::"memory");
+    asm volatile("s_waitcnt vmcnt(0)\n\t; qvit_pin %0 %1 %2 %3 %4"
+                 : "+v"(wpre[0]), "+v"(wpre[1]), "+v"(wpre[2]), "+v"(wpre[3]), "+v"(wpre[4])::"memory");
 #pragma unroll
     for (int k = 0; k < WPT; ++k) {
-      const int i = tid + 512 * k, o = i / per, c16 = i - o * per;
+      const int i = tid + 512 * k, o = head ? i >> 2 : i / 36, c16 = i - o * per;
       if (i < rows * per) *reinterpret_cast<v4i*>(wl + o * stride + 16 * c16) = wpre[k];
     }
   };
@@ -881,15 +886,15 @@ __global__ __launch_bounds__(512, 1) void ultra_tail_kernel(const int8_t* __rest
     bn_l[l][0][c] = ta.alpha[l][c];
     bn_l[l][1][c] = ta.shift[l][c];
   }
-  fetch_w(ta.w[0], 64, 9 * 64, kpad);
-  put_w(64, 9 * 64, TL_WSTR);
+  fetch_w(ta.w[0], false, kpad);
+  put_w(false);
   __syncthreads();
 
   for (int l = 0; l < 4; ++l) {
     const int8_t* src = (l & 1) ? imgB : imgA;
     int8_t* dst = (l & 1) ? imgA : imgB;
-    if (l < 3) fetch_w(ta.w[l + 1], 64, 9 * 64, kpad);  // lands while this layer computes
-    else fetch_w(hw, 48, 64, hkpad);
+    const bool head = l == 3;
+    fetch_w(head ? hw : ta.w[l < 3 ? l + 1 : 3], head, head ? hkpad : kpad);  // lands while this layer computes
     // the wave's patches P = wave + 8 k (k < TL_PW) all at once: each weight fragment read feeds TL_PW patches
     v4i acc[TL_PW][4];
 #pragma unroll
@@ -945,8 +950,7 @@ __global__ __launch_bounds__(512, 1) void ultra_tail_kernel(const int8_t* __rest
       }
     }
     __syncthreads();  // every read of this layer's weights and source image done, dst complete
-    if (l < 3) put_w(64, 9 * 64, TL_WSTR);
-    else put_w(48, 64, TL_HSTR);
+    put_w(head);
     __syncthreads();
   }
 

@@ -118,10 +118,15 @@ def _round_up(v: int, m: int) -> int:
     return (v + m - 1) // m * m
 
 
-# The int path's W4 GEMMs (qvit_gemm, qvit_gemm_qkv_split) take the register-weight image of the packed codes
-# (qvit_pack_weight_w4r: same results, each GEMM wave's weight rows loaded into registers instead of through LDS;
-# round 5: fc1 -2.6 % in the model). QVIT_GEMM_W4R=0 keeps the LDS-staged form (same-box A/B).
-GEMM_W4R = os.environ.get("QVIT_GEMM_W4R", "1") == "1"
+# The int path's W4 GEMMs (qvit_gemm, qvit_gemm_qkv_split) take a register image of the packed codes (same
+# results, each GEMM wave's weight rows loaded into registers instead of through LDS): "w4r" (qvit_pack_weight_w4r,
+# the int4 bytes re-ordered; round 5: fc1 -2.6 % in the model) or "w8r" (qvit_pack_weight_w8r, the codes already
+# unpacked to the MFMA's int8 operands: twice the bytes, no unpack in the main loop). QVIT_GEMM_WREG=w4 (or the
+# older QVIT_GEMM_W4R=0) keeps the LDS-staged form (same-box A/B).
+GEMM_WREG = os.environ.get("QVIT_GEMM_WREG", "w4r" if os.environ.get("QVIT_GEMM_W4R", "1") == "1" else "w4")
+if GEMM_WREG not in ("w4", "w4r", "w8r"):
+    raise ValueError(f"QVIT_GEMM_WREG={GEMM_WREG!r}: expected w4, w4r or w8r")
+GEMM_W4R = GEMM_WREG != "w4"   # a register image is in use
 
 
 @dataclass
@@ -150,9 +155,10 @@ class QuantPlan:
     extra: dict = field(default_factory=dict)
 
     def gemm_weights(self) -> Tuple[torch.Tensor, int]:
-        """(image, wfmt) the int path's GEMM reads: the W4R image when the plan holds one, else the packed codes."""
-        w4r = self.extra.get("w4r")
-        return (w4r, _lib.W4R) if w4r is not None else (self.packed, self.wfmt)
+        """(image, wfmt) the int path's GEMM reads: the register image (W4R / W8R) when the plan holds one, else
+        the packed codes."""
+        wreg = self.extra.get("wreg")
+        return wreg if wreg is not None else (self.packed, self.wfmt)
 
 
 class QuantizeMixin:
@@ -340,8 +346,10 @@ class QuantizeMixin:
                 packed = _lib.pack_weight(w32, qt_pack, d_pack, qm_pack, t_pack, wfmt, npad, kpad, overflow)
                 if int(overflow.item()) == 0:
                     plan.packed, plan.wfmt, plan.int_path = packed, wfmt, True
-                    if wfmt == _lib.W4 and GEMM_W4R:
-                        plan.extra["w4r"] = _lib.pack_weight_w4r(packed, npad, kpad)
+                    if wfmt == _lib.W4 and GEMM_WREG == "w4r":
+                        plan.extra["wreg"] = (_lib.pack_weight_w4r(packed, npad, kpad), _lib.W4R)
+                    elif wfmt == _lib.W4 and GEMM_WREG == "w8r":
+                        plan.extra["wreg"] = (_lib.pack_weight_w8r(packed, npad, kpad), _lib.W8R)
                     break
         if not plan.int_path and abs(lw) <= 65536:
             # fp32 activations against the packed weight codes (qvit_gemm_wonly, QuantizeLinear): the weight-only

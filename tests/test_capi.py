@@ -83,6 +83,15 @@ def test_argument_validation_without_launch(lib):
     assert lib.qvit_pack_weight_w4r(fake, 256, 128, ctypes.c_void_p(0x2008), None) == -2
     assert lib.qvit_pack_weight_w4r(fake, 256, 128, fake, None) == -1
     assert lib.qvit_pack_weight_w4r(None, 256, 128, other, None) == -3
+    # the int8 register image: the same argument rules
+    assert lib.qvit_pack_weight_w8r(fake, 100, 128, other, None) == -1
+    assert lib.qvit_pack_weight_w8r(fake, 256, 100, other, None) == -1
+    assert lib.qvit_pack_weight_w8r(fake, 256, 65536 + 128, other, None) == -1
+    assert lib.qvit_pack_weight_w8r(fake, 256, 128, ctypes.c_void_p(0x2008), None) == -2
+    assert lib.qvit_pack_weight_w8r(fake, 256, 128, fake, None) == -1
+    assert lib.qvit_pack_weight_w8r(None, 256, 128, other, None) == -3
+    assert lib.qvit_gemm(fake, 16, 65536 + 128, 65536 + 128, fake, _lib.W8R, 16, 256, fake, fake, None, 0, fake, 16,
+                         0, None, None, None, 0, None, None) == -1
     # QVIT_W4R: the int4 accumulation bound applies; the fused residual + LayerNorm GEMM takes W4 / W8 only
     assert lib.qvit_gemm(fake, 16, 65536 + 128, 65536 + 128, fake, _lib.W4R, 16, 256, fake, fake, None, 0, fake, 16,
                          0, None, None, None, 0, None, None) == -1

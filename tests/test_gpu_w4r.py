@@ -1,5 +1,6 @@
-"""The register-weight GEMM path (QVIT_W4R: qvit_pack_weight_w4r image, each wave's weight rows loaded into
-registers) against the LDS-staged QVIT_W4 path on the same codes: byte-identical outputs for every epilogue,
+"""The register-weight GEMM paths (QVIT_W4R: qvit_pack_weight_w4r image; QVIT_W8R: qvit_pack_weight_w8r image, the
+codes as 16x-scaled int8 operands; each wave's weight rows loaded into registers) against the LDS-staged QVIT_W4
+path on the same codes: byte-identical outputs for every epilogue,
 including the tile schedules the two paths sequence differently (K = 128: no steady step; K = 256: the peeled
 steps of the fp32 epilogues; row and column tails; several tiles per workgroup), and for the qkv split GEMM.
 The W4 path itself is pinned to the oracle by test_gpu_kernels.py."""
@@ -30,15 +31,25 @@ def _run(dev, wimg, wfmt, A, M, kpad, N, npad, bias_pad, epi, base, table, q):
     return C
 
 
+def _reg_image(packed, npad, kpad, wfmt):
+    if wfmt == _lib.W4R:
+        img = _lib.pack_weight_w4r(packed, npad, kpad)
+        assert img.numel() == packed.numel()
+    else:
+        img = _lib.pack_weight_w8r(packed, npad, kpad)
+        assert img.numel() == 2 * packed.numel()
+    return img
+
+
+@pytest.mark.parametrize("wreg", [_lib.W4R, _lib.W8R])
 @pytest.mark.parametrize("epi", EPIS)
 @pytest.mark.parametrize("M,N,K", SHAPES)
-def test_gemm_w4r_equals_w4(dev, epi, M, N, K):
+def test_gemm_w4r_equals_w4(dev, epi, M, N, K, wreg):
     g = torch.Generator().manual_seed(M * 3 + N * 5 + K * 7 + epi)
     a = torch.randint(-127, 128, (M, K), generator=g)
     w = torch.randint(-8, 8, (N, K), generator=g)
     packed, npad, kpad = pack_codes(w, _lib.W4, dev)
-    w4r = _lib.pack_weight_w4r(packed, npad, kpad)
-    assert w4r.numel() == packed.numel()
+    w4r = _reg_image(packed, npad, kpad, wreg)
     A = act_buffer(a, kpad, dev)
     bias_pad = _lib.pad_bias((torch.randn(N, generator=g) * 0.3).to(dev), N, npad, dev)
     base = torch.randn(M, _round_up(N, 4), generator=g).to(dev)
@@ -49,22 +60,23 @@ def test_gemm_w4r_equals_w4(dev, epi, M, N, K):
         geo = epilogue_table_geometry(qt, dn, qmn, t, saturation_level(qt, dn, qmn, t), epi == _lib.EPI_I8_GELU)
         table = _lib.epi_table_build(epi, qt, q["out_d"], q["out_qm"], q["out_t"], 0, *geo, dev)
     ref = _run(dev, packed, _lib.W4, A, M, kpad, N, npad, bias_pad, epi, base, table, q)
-    got = _run(dev, w4r, _lib.W4R, A, M, kpad, N, npad, bias_pad, epi, base, table, q)
+    got = _run(dev, w4r, wreg, A, M, kpad, N, npad, bias_pad, epi, base, table, q)
     assert torch.equal(got, ref)
 
 
+@pytest.mark.parametrize("wreg", [_lib.W4R, _lib.W8R])
 @pytest.mark.parametrize("B,seq,H,K", [(3, 197, 12, 768), (2, 50, 4, 768), (1, 577, 16, 1024)])
-def test_gemm_qkv_split_w4r_equals_w4(dev, B, seq, H, K):
+def test_gemm_qkv_split_w4r_equals_w4(dev, B, seq, H, K, wreg):
     g = torch.Generator().manual_seed(B + seq + H)
     M, N = B * seq, 3 * H * 64
     a = torch.randint(-127, 128, (M, K), generator=g)
     w = torch.randint(-8, 8, (N, K), generator=g)
     packed, npad, kpad = pack_codes(w, _lib.W4, dev)
-    w4r = _lib.pack_weight_w4r(packed, npad, kpad)
+    w4r = _reg_image(packed, npad, kpad, wreg)
     A = act_buffer(a, kpad, dev)
     bias_pad = _lib.pad_bias(torch.randn(N, generator=g).to(dev), N, npad, dev)
     outs = []
-    for img, wf in ((packed, _lib.W4), (w4r, _lib.W4R)):
+    for img, wf in ((packed, _lib.W4), (w4r, wreg)):
         hi = torch.empty(M * N, dtype=torch.float16, device=dev)
         lo = torch.empty(M * N, dtype=torch.float16, device=dev)
         _lib.gemm_qkv_split(A, M, kpad, img, wf, N, npad, _p(0.004, dev), _p(0.0011, dev), bias_pad, seq, 0.5,
@@ -75,10 +87,10 @@ def test_gemm_qkv_split_w4r_equals_w4(dev, B, seq, H, K):
 
 
 def test_quant_linear_plan_holds_w4r(dev):
-    """The module path runs its int GEMMs on the W4R image (quant_layers.GEMM_W4R) and matches the W4 form."""
+    """The module path runs its int GEMMs on the register image (quant_layers.GEMM_WREG) and matches the W4 form."""
     from quantized_vit_amd import quant_layers as QL
     if not QL.GEMM_W4R:
-        pytest.skip("QVIT_GEMM_W4R=0")
+        pytest.skip("QVIT_GEMM_WREG=w4")
     torch.manual_seed(0)
     lin = QL.QuantizeLinear.from_module(torch.nn.Linear(768, 3072).to(dev), num_bits=4,
                                         quant_mode=QL.QuantizationMode.WEIGHT_AND_ACTIVATION).eval()
@@ -86,10 +98,11 @@ def test_quant_linear_plan_holds_w4r(dev):
         x = torch.randn(300, 768, device=dev)
         y = lin(x)
         plan = lin.quant_plan()
-        assert plan.int_path and plan.wfmt == _lib.W4 and plan.extra.get("w4r") is not None
-        w4r = plan.extra.pop("w4r")
+        assert plan.int_path and plan.wfmt == _lib.W4 and plan.extra.get("wreg") is not None
+        assert plan.extra["wreg"][1] == {"w4r": _lib.W4R, "w8r": _lib.W8R}[QL.GEMM_WREG]
+        w4r = plan.extra.pop("wreg")
         try:
             y4 = lin(x)
         finally:
-            plan.extra["w4r"] = w4r
+            plan.extra["wreg"] = w4r
     assert torch.equal(y, y4)

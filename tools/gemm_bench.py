@@ -26,6 +26,10 @@ SHAPES = {
     "fc1": (M_B256, 3072, 768, _lib.EPI_I8_GELU),
     "fc1_a32": (M_B256, 3072, 768, _lib.EPI_I8_GELU),   # qvit_gemm_a32 on T32 codes (the fused block's fc1)
     "fc1_f32": (M_B256, 3072, 768, _lib.EPI_F32),
+    # fc1 at row counts whose 12 x ceil(M / 128) tiles fill whole rounds of the 512 resident blocks (49 152: 9.00)
+    # or not (50 432, the b256 shape: 9.23; 53 248: 9.75): the cost of the ragged last round
+    "fc1_9r": (49152, 3072, 768, _lib.EPI_I8_GELU),
+    "fc1_975r": (53248, 3072, 768, _lib.EPI_I8_GELU),
     "fc1_i32": (M_B256, 3072, 768, _lib.EPI_I32),
     "fc1_i8": (M_B256, 3072, 768, _lib.EPI_I8),
     "fc1_i8nt": (M_B256, 3072, 768, _lib.EPI_I8),   # no code table: per-element quantizer
@@ -41,9 +45,12 @@ def p(v, dev):
     return torch.tensor([float(v)], device=dev)
 
 
-def run(name, M, N, K, epi, iters, dev, qtype=_lib.QT_NONLINEAR):
+def run(name, M, N, K, epi, iters, dev, qtype=_lib.QT_NONLINEAR, act_std=0.0):
     npad = (N + _lib.TILE_N - 1) // _lib.TILE_N * _lib.TILE_N
-    A = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
+    if act_std > 0:   # model-like codes (LayerNorm outputs: roughly normal), which hold a higher clock than full-range
+        A = (torch.randn(M, K, device=dev) * act_std).round().clamp(-127, 127).to(torch.int8)
+    else:
+        A = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
     packed = torch.randint(0, 256, (npad * K // 2,), dtype=torch.uint8, device=dev)
     bias = torch.randn(npad, device=dev) * 0.01
     if epi in (_lib.EPI_I8, _lib.EPI_I8_GELU):
@@ -68,11 +75,15 @@ def run(name, M, N, K, epi, iters, dev, qtype=_lib.QT_NONLINEAR):
         tab = _lib.epi_table_build(_lib.EPI_I8, qtype, kw["out_d"], kw["out_qm"], kw["out_t"], 0, *geo, dev)
 
     A32 = _lib.rows_to_t32(A, K) if name.endswith("a32") else None
-    # the product's form of the int4 weights (quant_layers.GEMM_W4R) when the loaded library has it; random bytes
-    # either way, so no repacking is needed for timing
+    # the product's form of the int4 weights (quant_layers.GEMM_WREG: w4r / w8r / w4) when the loaded library has it;
+    # random bytes either way, so no repacking is needed for timing
     wfmt = _lib.W4
-    if os.environ.get("QVIT_GEMM_W4R", "1") == "1" and hasattr(_lib.load(), "qvit_pack_weight_w4r"):
+    wreg = os.environ.get("QVIT_GEMM_WREG", "w4r" if os.environ.get("QVIT_GEMM_W4R", "1") == "1" else "w4")
+    if wreg == "w4r" and hasattr(_lib.load(), "qvit_pack_weight_w4r"):
         wfmt = _lib.W4R
+    elif wreg == "w8r" and hasattr(_lib.load(), "qvit_pack_weight_w8r"):
+        wfmt = _lib.W8R
+        packed = torch.randint(0, 16, (npad * K,), dtype=torch.uint8, device=dev) * 16  # 16 w bytes
 
     def launch():
         if epi == -1:
@@ -104,6 +115,7 @@ def main():
     ap.add_argument("--shapes", default="qkv,proj,fc1,fc1_f32,fc1_i32,fc1_i8,fc2")
     ap.add_argument("--json", default=None)
     ap.add_argument("--lib", default="", help="time another build of the library (same-box A/B)")
+    ap.add_argument("--act-std", type=float, default=0.0, help="normal activation codes of this std (0: full range)")
     a = ap.parse_args()
     if a.lib:
         _lib.load(a.lib)
@@ -112,7 +124,7 @@ def main():
     res = []
     for name in a.shapes.split(","):
         M, N, K, epi = SHAPES[name]
-        r = run(name, M, N, K, epi, a.iters, dev)
+        r = run(name, M, N, K, epi, a.iters, dev, act_std=a.act_std)
         res.append(r)
         print(f"{name:8s} M={M:6d} N={N:5d} K={K:5d} epi={epi}  {r['ms']*1e3:8.1f} us  {r['tops']:7.1f} TOPS  "
               f"{100*r['frac']:5.1f}% of int8 peak", flush=True)

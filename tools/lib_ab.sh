@@ -11,7 +11,7 @@ export TMPDIR=/tmp
 for r in $(seq 1 "$ROUNDS"); do
   for lib in "$@"; do
     tag=$(basename "$lib" .so)
-    timeout -k 10 240 python tools/gemm_bench.py --iters 20 --shapes "$SHAPES" --lib "$lib" > "$OUT/g_${tag}_$r.log" 2>&1 \
+    timeout -k 10 240 python tools/gemm_bench.py --iters 20 ${ACT_STD:+--act-std $ACT_STD} --shapes "$SHAPES" --lib "$lib" > "$OUT/g_${tag}_$r.log" 2>&1 \
       || { echo "gemm_bench $tag failed"; tail -5 "$OUT/g_${tag}_$r.log"; exit 1; }
     echo "== gemm $tag round $r"; grep -v '^{' "$OUT/g_${tag}_$r.log" | tail -8
   done
