@@ -546,9 +546,16 @@ __global__ __launch_bounds__(NW_WAVES * 64) void conv_wonly_narrow_kernel(
 struct NarrowGeo {
   int nke, nt;
 };
-NarrowGeo narrow_geo(int wfmt, int64_t N, int64_t npad, int64_t kreal, int64_t K, int64_t H, int64_t W) {
+NarrowGeo narrow_geo(int wfmt, int64_t N, int64_t npad, int64_t K, const WoConv& cg) {
   if (!g_wonly_narrow || (wfmt != QVIT_W4 && wfmt != QVIT_W8) || N > 64 || npad < 64) return {0, 0};
-  if (H >= 32767 || W >= 32767) return {0, 0};  // (tap offsets dy, dx packed in 16 bits)
+  // the tap table holds each tap's input offset (c H + dy) W + dx as an int32 and dy, dx in 16 bits each, with
+  // dy = 0x7fff marking a zero tap (never inside the image: iy0 + 0x7fff >= H for every iy0 >= -ph); layers past
+  // these bounds take the wide schedule, which computes the offsets in 64 bits
+  const int64_t dy_max = (int64_t)cg.dh * (cg.kh - 1), dx_max = (int64_t)cg.dw * (cg.kw - 1);
+  if (cg.H >= 32767 || cg.W >= 32767 || dy_max >= 32767 || dx_max >= 32767) return {0, 0};
+  if ((int64_t)cg.ph + cg.H > 32767) return {0, 0};
+  if ((int64_t)cg.C * cg.H * cg.W + dy_max * cg.W + dx_max > INT32_MAX) return {0, 0};
+  const int64_t kreal = cg.kreal;
   const int nke = (int)((kreal + WO_BK - 1) / WO_BK);
   const int nt = (int)((N + 15) / 16);
   const int wrow = wfmt == QVIT_W4 ? 32 : 64;
@@ -608,7 +615,7 @@ int wonly_launch(const float* X, int64_t M, int64_t K, int64_t ldx, const void* 
   const int64_t ntiles = (npad / WO_BN) * ((M + WO_BM - 1) / WO_BM);
   if (ntiles > INT32_MAX / 2) return QVIT_EINVAL;
   if (CONV) {  // few output channels: the narrow schedule
-    const NarrowGeo g = narrow_geo(wfmt, N, npad, cg.kreal, K, cg.H, cg.W);
+    const NarrowGeo g = narrow_geo(wfmt, N, npad, K, cg);
     if (g.nke > 0)
       return narrow_launch<0>(g, X, M, reinterpret_cast<const int8_t*>(Wp), wfmt, N, d_wt, bias, nullptr, nullptr,
                               0.f, Y, cg, stream);
@@ -713,8 +720,9 @@ extern "C" int qvit_conv_wonly_bn_act(const float* X, int64_t B, int64_t C, int6
   if (st != QVIT_OK) return st;
   if (!bn_alpha || !bn_shift) return QVIT_ENULL;
   if (a_levels < 1 || a_levels > 127) return QVIT_EINVAL;
-  const NarrowGeo g = narrow_geo(wfmt, N, npad, cg.kreal, K, cg.H, cg.W);
-  if (g.nke == 0) return QVIT_EINVAL;  // (N > 64, W16 / W24, or a weight panel past NW_WMAX: unfused modules)
+  const NarrowGeo g = narrow_geo(wfmt, N, npad, K, cg);
+  // (N > 64, W16 / W24, a weight panel past NW_WMAX, or offsets past the tap table's bounds: unfused modules)
+  if (g.nke == 0) return QVIT_EINVAL;
   if (M == 0) return QVIT_OK;
   return narrow_launch<1>(g, X, M, reinterpret_cast<const int8_t*>(Wp), wfmt, N, d_wt, bias, bn_alpha, bn_shift,
                           (float)a_levels, Y, cg, stream);

@@ -216,8 +216,11 @@ class UltraNetQua(nn.Module):
         """mymodel.py:134-144 module by module: Conv2d_Q on qvit_conv_wonly, activation_quantize_fn on the HIP
         quantizer; BatchNorm2d and MaxPool2d on ATen's own kernels (the MIOpen batch-norm route off, so no
         library kernel is on the path). In eval mode each Conv2d_Q -> BatchNorm2d -> activation_quantize_fn triple
-        runs as one launch (Conv2d_Q.forward_bn_act: the BN applied as the fused network folds it); the
-        Sequential's own forward hooks are not called on this walk. Any image size, training mode included; under autograd (grad mode on and a
+        runs as one launch (Conv2d_Q.forward_bn_act: the BN applied as the fused network folds it, fma(y, alpha,
+        shift), which is not ATen's (x - mean) * invstd * w + b bit for bit: a 4-bit code can flip at a rounding tie,
+        inside the 1e-3 end-to-end bar) unless one of the three modules carries forward (pre-)hooks or global module
+        hooks are registered, which then run module by module as usual; the Sequential's own forward hooks are not
+        called on this walk. Any image size, training mode included; under autograd (grad mode on and a
         parameter or the input requiring grad) the Conv2d_Q layers take the reference's F.conv2d on the fake-quant
         weight instead, so gradients flow (the packed-codes kernels record no history)."""
         img_size = x.shape[-2:]
@@ -226,7 +229,7 @@ class UltraNetQua(nn.Module):
             mods, i = list(self.layers), 0
             while i < len(mods):
                 m = mods[i]
-                if hasattr(m, "forward_bn_act") and i + 2 < len(mods):
+                if hasattr(m, "forward_bn_act") and i + 2 < len(mods) and not _hooked(mods[i:i + 3]):
                     y = m.forward_bn_act(x, mods[i + 1], mods[i + 2])   # conv -> BN -> quantizer in one launch
                     if y is not None:
                         x, i = y, i + 3
@@ -238,6 +241,15 @@ class UltraNetQua(nn.Module):
             return yolo_out
         io, p = zip(*yolo_out)
         return torch.cat(io, 1), p
+
+
+def _hooked(mods) -> bool:
+    """Whether a forward (pre-)hook would see any of these modules' calls (their own hooks or global ones): the
+    fused conv -> BN -> quantizer launch would skip them."""
+    from torch.nn.modules import module as _m
+    if _m._global_forward_hooks or _m._global_forward_pre_hooks:
+        return True
+    return any(mod._forward_hooks or mod._forward_pre_hooks for mod in mods)
 
 
 def synthetic_images_u8(batch: int, size: int = 416, seed: int = 0, device=None) -> torch.Tensor:

@@ -97,3 +97,18 @@ def test_argument_validation_without_launch(lib):
                          0, None, None, None, 0, None, None) == -1
     # zero-size work is a no-op success
     assert lib.qvit_quantize_act_i8(fake, 0, 16, 16, 0, fake, fake, None, 0, fake, 16, 16, None) == 0
+
+
+def test_conv_wonly_bn_act_rejects_offsets_past_the_tap_table(lib):
+    """The narrow conv schedule keeps each tap's input offset in 32 bits and dy, dx in 16: inputs past
+    those bounds are refused by the narrow-only fused entry (the module falls back to its unfused path) and take the
+    wide schedule in qvit_conv_wonly. Checked before any launch."""
+    fake = ctypes.c_void_p(0x1000)
+
+    def call(C, H, W, kh=3, kw=3, ph=1, pw=1, dh=1, dw=1):
+        return lib.qvit_conv_wonly_bn_act(fake, 1, C, H, W, kh, kw, 1, 1, ph, pw, dh, dw, fake, _lib.W4, 16, 256,
+                                          (C * kh * kw + 127) // 128 * 128, fake, None, fake, fake, 15, fake, None)
+    assert call(64, 5800, 5800) == -1                       # C H W >= 2^31: an int32 tap offset would overflow
+    assert call(4, 100, 100, kh=2, dh=40000, ph=20000) == -1   # the tap's dy needs more than 15 bits
+    assert call(4, 100, 100, kw=2, dw=40000, pw=20000) == -1   # dx likewise
+    assert call(4, 100, 100, ph=32700) == -1                 # the zero-tap sentinel dy = 0x7fff could land inside

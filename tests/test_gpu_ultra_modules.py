@@ -335,3 +335,22 @@ def test_conv2d_q_invalidate_and_grad(dev):
     xg = x.clone().requires_grad_(True)
     conv(xg).sum().backward()             # grad mode: F.conv2d on quantize_fn(weight)
     assert xg.grad is not None and xg.grad.abs().sum().item() > 0
+
+
+def test_forward_modules_keeps_hooks(dev):
+    """A forward hook on a BatchNorm2d (hook-based calibration / feature capture) is called: with hooks present the
+    conv -> BN -> quantizer triple runs module by module instead of as the fused launch, and the hook
+    sees the BN output the unfused path computes."""
+    from quantized_vit_amd.ultranet import random_ultranet, synthetic_images_u8
+    model = random_ultranet(seed=2, device=dev, calib_batch=1, img_size=408)
+    img = synthetic_images_u8(1, 408, seed=9).to(dev)
+    bn = model.layers[1]
+    assert isinstance(bn, torch.nn.BatchNorm2d)
+    seen = []
+    h = bn.register_forward_hook(lambda mod, inp, out: seen.append(out.shape))
+    try:
+        with torch.no_grad():
+            model(img)
+    finally:
+        h.remove()
+    assert len(seen) == 1 and seen[0][1] == bn.num_features

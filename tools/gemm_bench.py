@@ -30,6 +30,12 @@ SHAPES = {
     # or not (50 432, the b256 shape: 9.23; 53 248: 9.75): the cost of the ragged last round
     "fc1_9r": (49152, 3072, 768, _lib.EPI_I8_GELU),
     "fc1_975r": (53248, 3072, 768, _lib.EPI_I8_GELU),
+    # the round staircase: one tile per block (12 tiles), one round (504 tiles), fc2 at 2.00 / 2.31 / 3.00 rounds
+    "fc1_1t": (128, 3072, 768, _lib.EPI_I8_GELU),
+    "fc1_1r": (5376, 3072, 768, _lib.EPI_I8_GELU),
+    "fc2_2r": (43648, 768, 3072, _lib.EPI_F32_RESID),
+    "fc2_3r": (65536, 768, 3072, _lib.EPI_F32_RESID),
+    "fc2_1t": (128, 768, 3072, _lib.EPI_F32_RESID),
     "fc1_i32": (M_B256, 3072, 768, _lib.EPI_I32),
     "fc1_i8": (M_B256, 3072, 768, _lib.EPI_I8),
     "fc1_i8nt": (M_B256, 3072, 768, _lib.EPI_I8),   # no code table: per-element quantizer
