@@ -92,9 +92,10 @@ def parse(argv=None):
 
 
 def _wreg() -> str:
-    """The weight image the int path's W4 GEMMs run on (quant_layers.GEMM_WREG): ", W4R>", ", W8R>" or ">"."""
+    """The weight image the int path's W4 GEMMs run on (quant_layers.GEMM_WREG), and the two-ahead activation ring
+    the register-weight GEMMs take at K >= 256: ", W4R, L2>", ", W8R, L2>" or ">"."""
     from quantized_vit_amd import quant_layers
-    return {"w4r": ", W4R>", "w8r": ", W8R>"}.get(quant_layers.GEMM_WREG, ">")
+    return {"w4r": ", W4R, L2>", "w8r": ", W8R, L2>"}.get(quant_layers.GEMM_WREG, ">")
 
 
 def _free_port() -> int:

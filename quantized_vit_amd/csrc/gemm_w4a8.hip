@@ -42,6 +42,12 @@ constexpr int BN = 256;    // weight rows per tile
 constexpr int BK = 64;     // k per stage
 constexpr int KTILE = 128; // the API's K granularity (QVIT_TILE_K): stages come in pairs
 constexpr int RING = 3;    // LDS stages
+#ifndef QVIT_GEMM_ALEAD
+#define QVIT_GEMM_ALEAD 2
+#endif
+// register-weight GEMMs (L2 below): activation stages in flight ahead of the one being read (ring of ALEAD + 2)
+constexpr int ALEAD = QVIT_GEMM_ALEAD;
+static_assert(ALEAD == 2 || ALEAD == 3, "the tail steps are written out for 2 or 3");
 // stages in flight ahead of the one being computed: 2 (the tail steps of a tile issue the next
 // tile's stages 0 and 1; the steady steps issue stage kt + 2)
 constexpr int EPI_LD = 68; // staged accumulator row pitch (ints): 64 + 4 pad
@@ -288,7 +294,7 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
   constexpr int XBYTES = G::XBYTES;
   constexpr bool I8OUT = (EPI == QVIT_EPI_I8 || EPI == QVIT_EPI_I8_GELU);
   static_assert(!L2 || RW != 0, "the two-ahead activation ring is for register weights");
-  constexpr int RINGN = L2 ? 4 : RING;                    // ring slots
+  constexpr int RINGN = L2 ? ALEAD + 2 : RING;            // ring slots
   constexpr int SLOT = L2 ? XBYTES : G::STAGE;            // bytes per slot
   constexpr int RING_B = RINGN * SLOT;
   __shared__ __attribute__((aligned(16))) int8_t smem[RING_B + G::EPI_BYTES + G::BIAS_BYTES + G::QP_BYTES];
@@ -593,7 +599,8 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     const uint32_t w0 = tile_w(t);
     issue(am0, w0, 0, 0);
     issue(am0, w0, 1, 1);
-    if constexpr (L2) issue(am0, w0, 2, 2);
+    if constexpr (L2)
+      for (int j = 2; j <= ALEAD; ++j) issue(am0, w0, j, j);
   }
   Frags<WFMT> fa, fb;
   QVIT_STAMP_DECL
@@ -610,96 +617,102 @@ __global__ __launch_bounds__((Geo<WFMT, WM>::NT), (Geo<WFMT, WM>::MIN_BLOCKS)) v
     }
 
     if constexpr (L2) {
-    // Two-ahead activation stream. Memory operations in issue order (XP = G::XPIECES, WREG per stage and wave):
-    // step kt issues w(kt + 1) then act(kt + 3), so the wait of step kt, which needs act(kt + 1) and w(kt), leaves
-    // exactly act(kt + 2), w(kt + 1), act(kt + 3) in flight: vmcnt(2 XP + WREG). The tail steps nk-3 .. nk-1 issue
-    // the next tile's stages 0 .. 2 in the place of act(kt + 3) (or nothing: the counts shrink by XP each).
-    // Ring slot safety: act(kt + 3) lands in the slot of stage kt - 1, whose fragments every wave read in step
-    // kt - 2, before the barrier of step kt - 1.
-    constexpr int DS = 2 * G::XPIECES + WREG;
+    // AL-ahead activation stream (AL = ALEAD: 2, or 3 in -DQVIT_GEMM_ALEAD=3 builds). Memory operations in issue
+    // order (XP = G::XPIECES activation pieces, WREG weight loads per stage and wave): step kt issues w(kt + 1), then
+    // act(kt + AL + 1) (this tile's, or in the tail steps nk-AL-1 .. nk-1 the next tile's stages 0 .. AL, or nothing).
+    // Step kt needs w(kt) (issued by step kt - 1, or the head for kt = 0) and act(kt + 1) (older than w(kt)): its
+    // wait leaves in flight exactly what was issued after w(kt) - step kt - 1's activation pieces and step kt's
+    // operations - so vmcnt(2 XP + WREG) in the steady steps, less where a step issues nothing of a kind.
+    // Ring slot safety (AL + 2 slots): act(kt + AL + 1) lands in the slot of stage kt - 1, whose fragments every wave
+    // read in step kt - 2, before the barrier of step kt - 1.
+    constexpr int XP = G::XPIECES;
     QVIT_STAMP(5);
     const uint32_t cw = tile_w(t);
     const int ln = lane_opaque();
     lane_offsets(ln);
     issue_w(cw, 0, fa);
     __builtin_amdgcn_s_waitcnt(0xC07F);
-    stage_sync<DS>();  // act(0): at most act(1), act(2), w(0) are younger and still in flight
+    stage_sync<ALEAD * XP + WREG>();  // act(0): at most act(1 .. AL) and w(0) are younger and still in flight
     QVIT_STAMP(0);
     QVIT_LSTAMP(0);
     if (has_bias && wave == 0)
       dma16(ep.bias + n0 + ln * 4, __builtin_amdgcn_readfirstlane(lds0 + RING_B + G::EPI_BYTES));
     read_frags(g % RINGN, fa);
-    // step 0 (accumulators start at zero when PEEL): needs act(1), w(0); younger: w(1), act(3)
+    // one step of this tile's stream: stage kt computes from cur, stage kt + 1's fragments are read into nxt
+    auto lstep = [&](int kt, Frags<WFMT>& cur, Frags<WFMT>& nxt, auto zeroc) __attribute__((always_inline)) {
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_sched_barrier(0);
+      issue_w(cw, kt + 1, nxt);
+      issue(m0, cw, kt + ALEAD + 1, (g + kt + ALEAD + 1) % RINGN);
+      QVIT_STAMP(1);
+      stage_sync<2 * XP + WREG>();
+      pin(cur);
+      QVIT_STAMP(2);
+      step_core(cur, nxt, (g + kt + 1) % RINGN, true, zeroc);
+      QVIT_STAMP(3);
+    };
+    // step 0 (accumulators start at zero when PEEL): needs act(1), w(0); younger: w(1), act(AL + 1)
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_sched_barrier(0);
     issue_w(cw, 1, fb);
-    issue(m0, cw, 3, (g + 3) % RINGN);
+    issue(m0, cw, ALEAD + 1, (g + ALEAD + 1) % RINGN);
     QVIT_STAMP(1);
-    stage_sync<G::XPIECES + WREG>();
+    stage_sync<XP + WREG>();
     pin(fa);
     QVIT_STAMP(2);
     if constexpr (PEEL) step_core(fa, fb, (g + 1) % RINGN, true, std::true_type{});
     else step_core(fa, fb, (g + 1) % RINGN, true, std::false_type{});
     QVIT_STAMP(3);
-    // steady steps 1 .. nk-4 in pairs (stage kt in fb, then kt + 1 in fa)
-    for (int kt = 1; kt + 1 <= nk - 4; kt += 2) {
-      __builtin_amdgcn_s_waitcnt(0xC07F);
-      __builtin_amdgcn_sched_barrier(0);
-      issue_w(cw, kt + 1, fa);
-      issue(m0, cw, kt + 3, (g + kt + 3) % RINGN);
-      QVIT_STAMP(1);
-      stage_sync<DS>();
-      pin(fb);
-      QVIT_STAMP(2);
-      step_core(fb, fa, (g + kt + 1) % RINGN, true, std::false_type{});
-      QVIT_STAMP(3);
-      __builtin_amdgcn_s_waitcnt(0xC07F);
-      __builtin_amdgcn_sched_barrier(0);
-      issue_w(cw, kt + 2, fb);
-      issue(m0, cw, kt + 4, (g + kt + 4) % RINGN);
-      QVIT_STAMP(1);
-      stage_sync<DS>();
-      pin(fa);
-      QVIT_STAMP(2);
-      step_core(fa, fb, (g + kt + 2) % RINGN, true, std::false_type{});
-      QVIT_STAMP(3);
+    // steady steps 1 .. nk-AL-2 (nk is even, so their count has AL's parity): an odd count starts with step 1
+    // alone, then pairs (stage kt in cur = kt odd ? fb : fa)
+    int kt = 1;
+    if constexpr (ALEAD & 1) {
+      lstep(1, fb, fa, std::false_type{});
+      kt = 2;
+      for (; kt + 1 <= nk - ALEAD - 2; kt += 2) {
+        lstep(kt, fa, fb, std::false_type{});
+        lstep(kt + 1, fb, fa, std::false_type{});
+      }
+    } else {
+      for (; kt + 1 <= nk - ALEAD - 2; kt += 2) {
+        lstep(kt, fb, fa, std::false_type{});
+        lstep(kt + 1, fa, fb, std::false_type{});
+      }
     }
-    // tail steps nk-3, nk-2, nk-1: the next tile's stages 0, 1, 2 (the weight loads go out before the branches,
-    // so every path from a load to its use holds a covering wait: tools/asm_load_check.py)
+    // tail steps j = 0 .. AL (kt = nk - AL - 1 + j): the next tile's stage j, if any; the weight load goes out before
+    // the branch, so every path from a load to its use holds a covering wait (tools/asm_load_check.py)
     const uint32_t nw = has_next ? tile_w(tnext) : 0u;
     const int nm0 = has_next ? tile_m0(tnext) : 0;
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_sched_barrier(0);
-    issue_w(cw, nk - 2, fa);
-    if (has_next) {
-      issue(nm0, nw, 0, (g + nk) % RINGN);
-      stage_sync<DS>();
+    auto tstep = [&](auto jc, Frags<WFMT>& cur, Frags<WFMT>& nxt) __attribute__((always_inline)) {
+      constexpr int j = decltype(jc)::value;
+      const int tk = nk - ALEAD - 1 + j;
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (j < ALEAD) issue_w(cw, tk + 1, nxt);
+      // younger than w(tk): the previous step's activation pieces (always issued before the tail, else only with a
+      // next tile), this step's weights and activation pieces
+      constexpr int NW = j < ALEAD ? WREG : 0;
+      if (has_next) {
+        issue(nm0, nw, j, (g + nk + j) % RINGN);
+        if constexpr (j < ALEAD) stage_sync<2 * XP + NW>();
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * XP) : "memory");
+      } else {
+        if constexpr (j < ALEAD) stage_sync<(j == 0 ? XP : 0) + NW>();
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      pin(cur);
+      step_core(cur, nxt, (g + tk + 1) % RINGN, j < ALEAD, std::false_type{});
+    };
+    if constexpr (ALEAD & 1) {   // nk - AL - 1 even: the tail starts in fa
+      tstep(std::integral_constant<int, 0>{}, fa, fb);
+      tstep(std::integral_constant<int, 1>{}, fb, fa);
+      tstep(std::integral_constant<int, 2>{}, fa, fb);
+      tstep(std::integral_constant<int, 3>{}, fb, fa);
     } else {
-      stage_sync<G::XPIECES + WREG>();
+      tstep(std::integral_constant<int, 0>{}, fb, fa);
+      tstep(std::integral_constant<int, 1>{}, fa, fb);
+      tstep(std::integral_constant<int, 2>{}, fb, fa);
     }
-    pin(fb);
-    step_core(fb, fa, (g + nk - 2) % RINGN, true, std::false_type{});
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_sched_barrier(0);
-    issue_w(cw, nk - 1, fb);
-    if (has_next) {
-      issue(nm0, nw, 1, (g + nk + 1) % RINGN);
-      stage_sync<DS>();
-    } else {
-      stage_sync<WREG>();
-    }
-    pin(fa);
-    step_core(fa, fb, (g + nk - 1) % RINGN, true, std::false_type{});
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_sched_barrier(0);
-    if (has_next) {
-      issue(nm0, nw, 2, (g + nk + 2) % RINGN);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G::XPIECES) : "memory");  // w(nk - 1); younger: next 1, 2
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    pin(fb);
-    step_core(fb, fa, 0, false, std::false_type{});
     QVIT_STAMP(3);
     QVIT_LSTAMP(1);
     } else {
@@ -1154,7 +1167,7 @@ int launch(const int8_t* A, int64_t M, int64_t K, int64_t lda, const void* Wp, i
       epc.ln_codes = ep.ln_codes + m0 * ep.ln_ldc;
     }
     // register weights and K >= 256 (4 stages or more per tile): the two-ahead activation ring
-    if (RW != 0 && K >= 256 && GEMM_L2)
+    if (RW != 0 && K / BK >= ALEAD + 2 && GEMM_L2)
       hipLaunchKernelGGL((gemm_kernel<WFMT, EPI, WMV, RW, RW != 0>), dim3((unsigned)grid), dim3(G::NT), 0, stream,
                          A + m0 * lda, (int)mc, (int)K, lda, reinterpret_cast<const int8_t*>(Wp), (int)N, (int)npad, Cc,
                          ldc, epc);

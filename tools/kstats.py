@@ -21,7 +21,7 @@ import re
 import statistics
 import sys
 
-FC1_KERNEL = re.compile(r"gemm_kernel<4, 2, 1(, (true|false))?>")  # W4 weights, I8_GELU epilogue, 4 waves (W4R or not)
+FC1_KERNEL = re.compile(r"gemm_kernel<4, 2, 1(, (true|false|\d))?(, (true|false))?>")  # W4 weights, I8_GELU epilogue, 4 waves (any weight image, ring)
 
 
 def top(path, n=25):

@@ -21,8 +21,8 @@ import re
 import statistics
 
 ROLES = {
-    "fc1": (re.compile(r"gemm_kernel<4, 2, 1(, (true|false))?>"), 1),
-    "resid": (re.compile(r"gemm_kernel<4, 1, 1(, (true|false))?>"), 2),
+    "fc1": (re.compile(r"gemm_kernel<4, 2, 1(, (true|false|\d))?(, (true|false))?>"), 1),
+    "resid": (re.compile(r"gemm_kernel<4, 1, 1(, (true|false|\d))?(, (true|false))?>"), 2),
     "qkv_attn": (re.compile(r"qkv_attn_kernel<"), 1),
     "ln": (re.compile(r"layernorm_quant_persist_kernel<"), 2),
 }
