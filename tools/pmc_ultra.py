@@ -13,9 +13,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=2)
+    ap.add_argument("--lib", default="", help="another build of the library (diagnostic variants)")
     a = ap.parse_args()
     from quantized_vit_amd import _lib
     from quantized_vit_amd.ultranet import random_ultranet, synthetic_images_u8
+    if a.lib:
+        _lib.load(a.lib)
     _lib.load()
     dev = torch.device("cuda", 0)
     model = random_ultranet(seed=0, device=dev)
