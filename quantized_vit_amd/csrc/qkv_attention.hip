@@ -38,9 +38,9 @@ constexpr int KV_BYTES = 4 * IMGF + 2048; // K hi, K lo, V hi, V lo + zero rows 
 constexpr int WGRP = 2048;                // one 64-row weight group of one k-step: 64 rows x 32 B (int4 image)
 constexpr int WSLOT = 3 * WGRP;           // q, k, v groups of one k-step: 6 DMA pieces
 constexpr int WRING = 4;                  // slots: k-step s computes from slot s % 4, s + 1 is read, s + 2, s + 3 land
-constexpr int WDIST = WRING - 1;          // weight k-steps issued ahead
 constexpr int XRING = 4;                  // activation register ring (k-steps s .. s + 3)
-constexpr int TOPCNT = 2 + 3 * (WDIST - 2);  // vmem ops a wave issues after its DMA piece of k-step s + 1
+// vmem ops a wave issues after its DMA piece of k-step s + 2 (s odd): the activation loads of k-steps s + 1, s + 2
+constexpr int TOPCNT = 2 * 2;
 constexpr int IMG4_STEP = 256 * 32;       // bytes of one (256-row tile, k-step) of the int4 weight image
 constexpr int TBL = 8192;                 // code table (<= 1022 buckets)
 constexpr int BIAS_MAX = 9216;            // fp32 bias of the qkv layer (<= 2304 features: H * 64 <= 768)
@@ -197,9 +197,9 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
   Src cur, nxt;
   unit_src(0, cur);
   unit_src(1, nxt);
-  // prologue: weight k-steps 0, 1 of the first unit, activation k-steps 0, 1, 2
+  // prologue: weight k-steps 0 .. 3 of the first unit, activation k-steps 0, 1, 2
 #pragma unroll
-  for (int t = 0; t < WDIST; ++t) dma_piece(cur, t, t);
+  for (int t = 0; t < WRING; ++t) dma_piece(cur, t, t);
   aoff[0] = cur.a[0];
   aoff[1] = cur.a[1];
   act_next(xa[0]);
@@ -219,7 +219,7 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
 
     // ---- 1. projection ---------------------------------------------------------------------------
     // unit head: everything issued before (the previous unit's output stores included) has landed, the
-    // ring slots of k-steps 0 and 1 are complete for every wave; read k-step 0's weight fragments
+    // ring slots of k-steps 0 .. 3 are complete for every wave; read k-step 0's weight fragments
     __builtin_amdgcn_s_waitcnt(0xC07F);
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     v4i acc[TPW][12];
@@ -230,27 +230,29 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
     uint2 wfr[12];
     // k-step s (ring slot and activation slot q = s % 4: nk % 4 == 0, so every unit starts at slot 0 and the
     // slot indices are compile-time constants in the 4-step groups):
-    //   top (s > 0): this wave's DMA piece of k-step s + 1 landed (TOPCNT = the activation loads and DMA
-    //   pieces issued after it may be in flight, which also covers the activations of k-step s), then the
-    //   barrier: k-step s + 1's slot is complete for everyone, and every wave is past k-step s - 1, the last
-    //   reader of slot (s + 3) % 4;
-    //   issue: weight k-step s + 3 -> slot (s + 3) % 4, activation k-step s + 3 -> register slot (s + 3) % 4
-    //   (past the unit's end: the next unit's k-steps 0, 1, 2);
+    //   top (s odd; one barrier per two k-steps): this wave's DMA pieces of k-steps s + 1 and s + 2 landed
+    //   (TOPCNT = the activation loads issued after them may be in flight, which also covers the activations
+    //   of k-step s), then the barrier: the slots of k-steps s + 1 (read during k-step s) and s + 2 (read
+    //   during k-step s + 1, before the next barrier) are complete for everyone, and every wave is past
+    //   k-step s - 1, the last reader of slots (s + 3) % 4 (k-step s - 1's) and (s + 4) % 4 (k-step s's);
+    //   issue (s odd): weight k-steps s + 3, s + 4 -> their slots; every k-step: activation k-step s + 3 ->
+    //   register slot (s + 3) % 4 (past the unit's end: the next unit's k-steps; at k-step 0 the unit head's
+    //   vmcnt(0) + barrier already cover k-steps 1 .. 3);
     //   MFMAs of k-step s: fragment f + 1 is unpacked while f's two MFMAs run, and each packed fragment is
     //   replaced by k-step s + 1's right after its MFMAs.
     // two: 2 when both of the wave's token tiles {2 wr, 2 wr + 1} are inside the image, else 1 (the second
-    // tile's MFMAs are skipped; N = 197 has 13 tiles). The order inside a k-step is pinned (sched_barrier); the DMA piece and the two
-    // activation loads go between the first fragments' MFMAs in that order (the next top's count).
+    // tile's MFMAs are skipped; N = 197 has 13 tiles). The order inside a k-step is pinned (sched_barrier); the DMA pieces (odd k-steps) and the
+    // two activation loads go between the first fragments' MFMAs in that order (the next top's count).
     auto kstep = [&](auto r0, auto r1, int s, int q) __attribute__((always_inline)) {
       constexpr int R0 = decltype(r0)::value, R1 = decltype(r1)::value;
       constexpr auto inr = [](int R, int f) constexpr { return R == 1 || (R == 2 && f < 6) || (R == 3 && f >= 6); };
       constexpr auto used = [=](int f) constexpr { return inr(R0, f) || inr(R1, f); };
       constexpr int F0 = (R0 == 3 && R1 != 1 && R1 != 2) ? 6 : 0;  // first fragment used
       __builtin_amdgcn_sched_barrier(0);
-      if (s > 0) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(TOPCNT) : "memory");
+      if (q & 1) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(TOPCNT) : "memory");
       __builtin_amdgcn_sched_barrier(0);
       sp.mark(7);
-      const int rd = (q + WDIST) & 3, rn = (q + 1) & 3;
+      const int rn = (q + 1) & 3;
       const bool more = s + 1 < nk;
       v4i wc = unpack16(wfr[F0]);
 #pragma unroll
@@ -259,9 +261,12 @@ __global__ __launch_bounds__(FT, 1) void qkv_attn_kernel(
         if (inr(R1, f)) acc[1][f] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wc, xa[q][1], acc[1][f], 0, 0, 0);
         if (f < 11 && used(f + 1)) wc = unpack16(wfr[f + 1]);
         if (more) wfr[f] = wfrag(rn, f);
-        if (f == 0) {  // weight k-step s + 3 (past the unit's end: the next unit's 0, 1, 2)
-          if (s + WDIST < nk) dma_piece(cur, s + WDIST, rd);
-          else dma_piece(nxt, s + WDIST - nk, rd);
+        if (f == 0 && (q & 1)) {  // weight k-steps s + 3, s + 4 (past the unit's end: the next unit's 0 .. 3)
+#pragma unroll
+          for (int d = 3; d <= 4; ++d) {
+            if (s + d < nk) dma_piece(cur, s + d, (q + d) & 3);
+            else dma_piece(nxt, s + d - nk, (q + d) & 3);
+          }
         }
         if (f == 2) {  // activation k-step s + 3 (past the unit's end: the next unit's 0, 1, 2)
           if (s + 3 == nk) {
