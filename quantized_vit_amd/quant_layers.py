@@ -155,10 +155,25 @@ class QuantPlan:
     extra: dict = field(default_factory=dict)
 
     def gemm_weights(self) -> Tuple[torch.Tensor, int]:
-        """(image, wfmt) the int path's GEMM reads: the register image (W4R / W8R) when the plan holds one, else
-        the packed codes."""
+        """(image, wfmt) the int path's GEMM reads: the register image (W4R / W8R) of a W4 plan, else the packed
+        codes. The register image is built on the first call and the packed codes it is made from are then
+        released, so a layer holds its int4 weights once (conv layers and the fused qkv + attention kernel never
+        call this and keep only the packed codes); `packed_codes()` re-packs them for a route that needs them."""
+        if self.int_path and self.wfmt == _lib.W4 and GEMM_WREG != "w4" and "wreg" not in self.extra:
+            src = self.packed_codes()
+            pack = _lib.pack_weight_w4r if GEMM_WREG == "w4r" else _lib.pack_weight_w8r
+            self.extra["wreg"] = (pack(src, self.npad, self.kpad), _lib.W4R if GEMM_WREG == "w4r" else _lib.W8R)
+            if self.extra.get("repack") is not None:
+                self.packed = None
         wreg = self.extra.get("wreg")
-        return wreg if wreg is not None else (self.packed, self.wfmt)
+        return wreg if wreg is not None else (self.packed_codes(), self.wfmt)
+
+    def packed_codes(self) -> torch.Tensor:
+        """The packed weight codes (qvit_pack_weight layout), re-packed from the layer's weights if
+        gemm_weights() released them (the same call that made them: deterministic, no overflow to re-check)."""
+        if self.packed is None:
+            self.packed = self.extra["repack"]()
+        return self.packed
 
 
 class QuantizeMixin:
@@ -346,10 +361,9 @@ class QuantizeMixin:
                 packed = _lib.pack_weight(w32, qt_pack, d_pack, qm_pack, t_pack, wfmt, npad, kpad, overflow)
                 if int(overflow.item()) == 0:
                     plan.packed, plan.wfmt, plan.int_path = packed, wfmt, True
-                    if wfmt == _lib.W4 and GEMM_WREG == "w4r":
-                        plan.extra["wreg"] = (_lib.pack_weight_w4r(packed, npad, kpad), _lib.W4R)
-                    elif wfmt == _lib.W4 and GEMM_WREG == "w8r":
-                        plan.extra["wreg"] = (_lib.pack_weight_w8r(packed, npad, kpad), _lib.W8R)
+                    if wfmt == _lib.W4:   # how gemm_weights() gets the packed codes back after releasing them
+                        plan.extra["repack"] = self._repacker(w2, codes, (qt_pack, d_pack, qm_pack, t_pack),
+                                                              wfmt, npad, kpad)
                     break
         if not plan.int_path and abs(lw) <= 65536:
             # fp32 activations against the packed weight codes (qvit_gemm_wonly, QuantizeLinear): the weight-only
@@ -382,6 +396,19 @@ class QuantizeMixin:
         if not plan.int_path and not plan.extra.get("wonly"):   # levels that fit neither int4 nor int8 (e.g. 16/32
             plan.w_fakequant = self._fake_quant_weight(plan)     # bits); the fp32 form is otherwise filled lazily
         return plan
+
+    @staticmethod
+    def _repacker(w2: torch.Tensor, codes: Optional[torch.Tensor], qargs: tuple, wfmt: int, npad: int, kpad: int):
+        """A closure that repeats quant_plan's packing of these weights (the fp32 source is re-derived on the call,
+        so the plan holds no fp32 copy)."""
+        def repack() -> torch.Tensor:
+            if codes is not None:
+                src = codes.to(device=w2.device, dtype=torch.float32).contiguous()
+            else:
+                src = w2 if (w2.dtype == torch.float32 and w2.is_contiguous()) else w2.float().contiguous()
+            overflow = torch.zeros(1, dtype=torch.int32, device=w2.device)
+            return _lib.pack_weight(src, *qargs, wfmt, npad, kpad, overflow)
+        return repack
 
     def _fake_quant_weight(self, plan: QuantPlan) -> torch.Tensor:
         """quantize_weight(W) on the device; with codes bound by load_weight_codes, d_w * k of exactly those
@@ -473,7 +500,7 @@ class QuantizeMixin:
         """gemm_codes for the int8-code epilogues on QVIT_ACT_T32 activation codes (qvit_gemm_a32: weight-stationary
         schedule, same codes as gemm_codes on the row-major codes)."""
         nplan = next_layer.quant_plan()
-        _lib.gemm_a32(codes_t32, M, plan.kpad, plan.packed, plan.wfmt, plan.n, plan.npad, plan.d_act, plan.d_wt,
+        _lib.gemm_a32(codes_t32, M, plan.kpad, plan.packed_codes(), plan.wfmt, plan.n, plan.npad, plan.d_act, plan.d_wt,
                       plan.bias_pad, epilogue, out, out_qtype=nplan.qtype, out_d=nplan.d_act, out_qm=nplan.qm_act,
                       out_t=nplan.t_act, epi_table=epilogue_table(nplan, epilogue))
         return out

@@ -265,7 +265,7 @@ class Block(nn.Module):
         quantizer -> int8 codes [M, p_next.kpad] (qvit_gemm_resid_ln: one launch)."""
         M, C = x2.shape
         out = torch.empty((M, p_next.kpad), dtype=torch.int8, device=x2.device)
-        _lib.gemm_resid_ln(codes_in, M, p_res.kpad, p_res.packed, p_res.wfmt, p_res.n, p_res.npad, p_res.d_act,
+        _lib.gemm_resid_ln(codes_in, M, p_res.kpad, p_res.packed_codes(), p_res.wfmt, p_res.n, p_res.npad, p_res.d_act,
                            p_res.d_wt, p_res.bias_pad, x2, norm.weight, norm.bias, norm.eps, p_next.qtype,
                            p_next.d_act, p_next.qm_act, p_next.t_act, 0, epilogue_table(p_next, _lib.EPI_I8), out,
                            p_next.kpad)
@@ -300,7 +300,7 @@ class Block(nn.Module):
                 out[:, a.num_heads * 64:].zero_()
             in_scale, tab = attention_in_scale(p_qkv), epilogue_table(p_proj, _lib.EPI_I8)
             with _timed("qkv_attn"):
-                _lib.qkv_attention(codes, B, N, p_qkv.kpad, p_qkv.packed, p_qkv.npad, p_qkv.d_act, p_qkv.d_wt,
+                _lib.qkv_attention(codes, B, N, p_qkv.kpad, p_qkv.packed_codes(), p_qkv.npad, p_qkv.d_act, p_qkv.d_wt,
                                    p_qkv.bias_pad, a.num_heads, a.scale, out, _lib.ATT_I8, in_scale,
                                    p_proj.qtype, p_proj.d_act, p_proj.qm_act, p_proj.t_act, epi_table=tab)
             trace_codes(a.proj, out, p_proj.k)

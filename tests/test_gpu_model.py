@@ -397,7 +397,7 @@ def stage_forced_block(model, cfg, sd, x, i, dev):
     if fused:
         # the production kernel: qkv projection + attention + proj's quantizer on the oracle's LN codes
         ca = torch.zeros((M, pp.kpad), dtype=torch.int8, device=dev)
-        _lib.qkv_attention(c, B, N, pq.kpad, pq.packed, pq.npad, pq.d_act, pq.d_wt, pq.bias_pad, a.num_heads,
+        _lib.qkv_attention(c, B, N, pq.kpad, pq.packed_codes(), pq.npad, pq.d_act, pq.d_wt, pq.bias_pad, a.num_heads,
                            a.scale, ca, _lib.ATT_I8, vit_model.attention_in_scale(pq), pp.qtype, pp.d_act, pp.qm_act,
                            pp.t_act, epi_table=epilogue_table(pp, _lib.EPI_I8))
         cmp_codes("fused qkv+attention codes", ca[:, :C], ao, "attn.proj")
@@ -406,7 +406,7 @@ def stage_forced_block(model, cfg, sd, x, i, dev):
         s_in = vit_model.attention_in_scale(pq)
         hi = torch.empty(M * pq.n, dtype=torch.float16, device=dev)
         lo = torch.empty_like(hi)
-        _lib.gemm_qkv_split(c, M, pq.kpad, pq.packed, pq.wfmt, pq.n, pq.npad, pq.d_act, pq.d_wt, pq.bias_pad, N,
+        _lib.gemm_qkv_split(c, M, pq.kpad, pq.packed_codes(), pq.wfmt, pq.n, pq.npad, pq.d_act, pq.d_wt, pq.bias_pad, N,
                             s_in, hi, lo)
         ca = torch.zeros((M, pp.kpad), dtype=torch.int8, device=dev)
         _lib.attention_split(hi, lo, B, N, a.num_heads, 64, a.scale, ca, _lib.ATT_I8, s_in, pp.qtype, pp.d_act,

@@ -87,7 +87,8 @@ def test_gemm_qkv_split_w4r_equals_w4(dev, B, seq, H, K, wreg):
 
 
 def test_quant_linear_plan_holds_w4r(dev):
-    """The module path runs its int GEMMs on the register image (quant_layers.GEMM_WREG) and matches the W4 form."""
+    """The module path runs its int GEMMs on the register image (quant_layers.GEMM_WREG), built on first use with the
+    packed codes then released (one int4 copy per layer), and matches the W4 form re-packed on demand."""
     from quantized_vit_amd import quant_layers as QL
     if not QL.GEMM_W4R:
         pytest.skip("QVIT_GEMM_WREG=w4")
@@ -100,9 +101,13 @@ def test_quant_linear_plan_holds_w4r(dev):
         plan = lin.quant_plan()
         assert plan.int_path and plan.wfmt == _lib.W4 and plan.extra.get("wreg") is not None
         assert plan.extra["wreg"][1] == {"w4r": _lib.W4R, "w8r": _lib.W8R}[QL.GEMM_WREG]
-        w4r = plan.extra.pop("wreg")
+        assert plan.packed is None
+        w4r, mode = plan.extra.pop("wreg"), QL.GEMM_WREG
+        QL.GEMM_WREG = "w4"
         try:
-            y4 = lin(x)
+            y4 = lin(x)   # the LDS-staged W4 GEMM on the re-packed codes
         finally:
+            QL.GEMM_WREG = mode
             plan.extra["wreg"] = w4r
+        assert plan.packed is not None
     assert torch.equal(y, y4)
