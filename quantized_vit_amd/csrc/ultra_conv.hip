@@ -120,7 +120,6 @@ typedef float c0f4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 QVIT_DEV float fmax_nn(float a, float b) { return __builtin_elementwise_maximum(a, b); }
-QVIT_DEV float fmin_nn(float a, float b) { return __builtin_elementwise_minimum(a, b); }
 // Tiles of this persistent block: with a grid that is a multiple of 8, XCD x (blocks x, x + 8, ...) owns a
 // contiguous tile range, so the tiles in flight on one XCD are neighbours whose halo rows share 128-B lines
 // in that XCD's L2 (walking t = blockIdx + k grid put x-neighbours on different XCDs: layer 0 fetched 3.2x
@@ -174,22 +173,27 @@ __global__ __launch_bounds__(256, C0_OCC) void ultra_conv0_mfma_kernel(const flo
 
   // B operands: weights [o = n][c][ky][kx] split hi / lo in the K order above; record r (0, 1) of group g is tap
   // (ky, kx) = g < 3 ? (g, r) : (r, 2)
+  // A channel whose BN decreases in the accumulator (alpha < 0) gets its B column negated: the hi / lo split
+  // and every product and sum are sign-symmetric, so its accumulators come out exactly negated, the max of
+  // them is minus the min of the true ones, and (-alpha) (-min) = alpha min. One max pool for every lane.
+  const float al = alpha[n], sh = shift[n];
+  const bool up = !(al < 0.f);  // BN increasing in the accumulator
+  const float alp = up ? al : -al;
   c0h8 wh0, wl0, wc1;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int r = j >> 2, c = j & 3;
     const int ky = g < 3 ? g : r, kx = g < 3 ? r : 2;
     const float w = c < 3 ? wvals[((n * 3 + c) * 3 + ky) * 3 + kx] : 0.f;
-    wh0[j] = hi_h(w);
-    wl0[j] = lo_h(w);
+    wh0[j] = up ? hi_h(w) : -hi_h(w);
+    wl0[j] = up ? lo_h(w) : -lo_h(w);
     const float w22 = c < 3 ? wvals[((n * 3 + c) * 3 + 2) * 3 + 2] : 0.f;
-    wc1[j] = g == 0 ? hi_h(w22) : (g == 1 && r == 0) ? lo_h(w22) : (_Float16)0;
+    const _Float16 c1 = g == 0 ? hi_h(w22) : (g == 1 && r == 0) ? lo_h(w22) : (_Float16)0;
+    wc1[j] = up ? c1 : -c1;
   }
-  const float al = alpha[n], sh = shift[n];
-  const bool up = !(al < 0.f);  // BN increasing in the accumulator
   // both BN constants arrive here, before the loop: a use inside the loop would otherwise carry a vmcnt(0) that
   // also drains the next tile's halo prefetch at the first patch
-  asm volatile("" ::"v"(al), "v"(sh));
+  asm volatile("" ::"v"(alp), "v"(sh));
 
   const int tiles_y = (H + C0_TY - 1) / C0_TY, tiles_x = (W + C0_TX - 1) / C0_TX;
   const int ntiles = B * tiles_y * tiles_x;
@@ -323,8 +327,7 @@ __global__ __launch_bounds__(256, C0_OCC) void ultra_conv0_mfma_kernel(const flo
 #pragma unroll
       for (int q = 0; q < C0_G; ++q) {
         const float mx = fmax_nn(fmax_nn(acc[q][0], acc[q][1]), fmax_nn(acc[q][2], acc[q][3]));
-        const float mn = fmin_nn(fmin_nn(acc[q][0], acc[q][1]), fmin_nn(acc[q][2], acc[q][3]));
-        const float y = __fadd_rn(__fmul_rn(up ? mx : mn, al), sh);
+        const float y = __fadd_rn(__fmul_rn(mx, alp), sh);
         const int code = (int)rintf(__builtin_amdgcn_fmed3f(y, 0.f, 1.f) * levels);
         cw[2 * (pq + q) * C0_OUT] = (int8_t)code;
       }
@@ -550,11 +553,26 @@ __global__ __launch_bounds__(256, STG ? 2 : CIN == 32 ? UC_MINB32 : CIN == 16 ? 
   const int py = SW ? 2 * (p >> 3) + ((p >> 1) & 1) : p >> 2;
   const int px = SW ? 2 * ((p >> 2) & 1) + (p & 1) : p & 3;
 
-  // weights -> LDS once per block (rows >= real cout are zero in the packed image)
+  // weights -> LDS once per block (rows >= real cout are zero in the packed image). STAGED with the BN path
+  // (OUT 0): the row of a channel whose BN decreases in the accumulator (alpha < 0) is stored negated (codes are
+  // in [-127, 127]), so its accumulators come out exactly negated and the pooled BN input is their max for every
+  // lane (acc_div is odd, and (-x)(-alpha) = x alpha): no min pool, no select (as ultra_conv0_mfma_kernel).
+  // (The unstaged pooled form, UltraNet's CIN 64 layer, measured slower with it: +4 %, profiles/r06_ultranet_bn_sign_fold_ab.txt)
+  constexpr bool NEG = STAGED && OUT == 0;
+  static_assert(!NEG || COUT <= 64, "one channel per lane of the sign ballot");
+  // bit o: channel o's BN decreases (one ballot per wave, so the staging loop reads no alpha)
+  const uint64_t negmask = NEG ? __ballot(lane < cout_real && alpha[lane < cout_real ? lane : 0] < 0.f) : 0;
   for (int i = tid; i < COUT * (G::KPAD / 16); i += 256) {
     const int o = i / (G::KPAD / 16), c16 = i % (G::KPAD / 16);
-    *reinterpret_cast<v4i*>(wl + o * G::WSTR + 16 * c16) =
-        *reinterpret_cast<const v4i*>(wcodes + (int64_t)o * kpad_in + 16 * c16);
+    v4i w = *reinterpret_cast<const v4i*>(wcodes + (int64_t)o * kpad_in + 16 * c16);
+    if (NEG && ((negmask >> o) & 1)) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {  // bytewise two's-complement negation: ~b + 1 without carries across bytes
+        const uint32_t t = ~(uint32_t)w[k];
+        w[k] = (int)(((t & 0x7f7f7f7fu) + 0x01010101u) ^ (t & 0x80808080u));
+      }
+    }
+    *reinterpret_cast<v4i*>(wl + o * G::WSTR + 16 * c16) = w;
   }
   float al[G::NCT][4], sh[G::NCT][4];
   int iinc[G::NCT][4], ibias[G::NCT][4];
@@ -574,7 +592,7 @@ __global__ __launch_bounds__(256, STG ? 2 : CIN == 32 ? UC_MINB32 : CIN == 16 ? 
 #pragma unroll
   for (int ct = 0; ct < G::NCT; ++ct) {
     const int o = 16 * ct + p;
-    als[ct] = (SW && OUT == 0 && o < cout_real) ? alpha[o] : 0.f;
+    als[ct] = (SW && OUT == 0 && o < cout_real) ? (NEG ? fabsf(alpha[o]) : alpha[o]) : 0.f;  // NEG: sign in the weights
     shs[ct] = (SW && OUT == 0 && o < cout_real) ? shift[o] : 0.f;
     iincs[ct] = (SW && OUT == 2 && o < cout_real) ? reinterpret_cast<const int*>(alpha)[o] : 0;
     ibiass[ct] = (SW && OUT == 2 && o < cout_real) ? reinterpret_cast<const int*>(shift)[o] : 0;
@@ -668,7 +686,7 @@ __global__ __launch_bounds__(256, STG ? 2 : CIN == 32 ? UC_MINB32 : CIN == 16 ? 
           const int vmax = max(max(v[0], v[1]), max(v[2], v[3]));
           const int vmin = min(min(v[0], v[1]), min(v[2], v[3]));
           const int code = (OUT == 2) ? int_code(iincs[ct] < 0 ? vmin : vmax, iincs[ct], ibiass[ct], sbits, (int)levels)
-                                      : act_code(acc_div(als[ct] < 0.f ? vmin : vmax, den, rden), als[ct], shs[ct], levels);
+                                      : act_code(acc_div(NEG || !(als[ct] < 0.f) ? vmax : vmin, den, rden), als[ct], shs[ct], levels);
           cw[2 * pt * COUT + 16 * ct] = (int8_t)code;
         }
       __builtin_amdgcn_wave_barrier();
@@ -720,7 +738,7 @@ __global__ __launch_bounds__(256, STG ? 2 : CIN == 32 ? UC_MINB32 : CIN == 16 ? 
           const int vmax = max(max(v[0], v[1]), max(v[2], v[3]));
           const int vmin = min(min(v[0], v[1]), min(v[2], v[3]));
           const int code = (OUT == 2) ? int_code(iincs[ct] < 0 ? vmin : vmax, iincs[ct], ibiass[ct], sbits, (int)levels)
-                                      : act_code(acc_div(als[ct] < 0.f ? vmin : vmax, den, rden), als[ct], shs[ct], levels);
+                                      : act_code(acc_div(NEG || !(als[ct] < 0.f) ? vmax : vmin, den, rden), als[ct], shs[ct], levels);
           const uint32_t word = pack_quad(code);  // channels 16 ct + p .. + 3 in lane p = 4k
           const int o = 16 * ct + p;
           if ((p & 3) == 0 && yo < Ho && xo < Wo && o < cout_real)

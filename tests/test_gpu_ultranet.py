@@ -73,6 +73,48 @@ def test_conv0_block_vs_oracle(dev, net):
     assert_codes(got, codes_of(trace[0]))
 
 
+@pytest.fixture(scope="module")
+def net_decreasing(dev):
+    """The test network with gamma < 0 in every other channel of every BatchNorm (BN decreasing in the
+    accumulator: a pooled code is that of the window's minimum; the pooled layers negate those channels' weights
+    and max-pool every lane), running statistics re-calibrated layer by layer as random_ultranet does."""
+    from quantized_vit_amd.ultranet import _aten_batch_norm
+    model = random_ultranet(seed=3, device=dev, calib_batch=2, img_size=416)
+    with torch.no_grad():
+        for m in model.layers:
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.weight[1::2] *= -1
+        x = synthetic_images_u8(2, 416, 4, dev)
+        with _aten_batch_norm():
+            for m in model.layers:
+                if isinstance(m, torch.nn.BatchNorm2d):
+                    m.running_mean.copy_(x.mean(dim=(0, 2, 3)))
+                    m.running_var.copy_(x.var(dim=(0, 2, 3)).clamp_min(1e-3))
+                x = m(x)
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    img = synthetic_images_u8(2, 416, seed=9)
+    trace = []
+    with torch.no_grad():
+        io, p = U.ultranet_forward(sd, img, trace=trace)
+    return model, sd, img, trace, io, p
+
+
+@pytest.mark.parametrize("k", range(0, 8))
+def test_decreasing_bn_stage_forced(dev, net_decreasing, k):
+    model, _, img, trace, _, _ = net_decreasing
+    plan, _ = model._build_plan(dev)
+    codes, alpha, shift, cout, pool = plan[k]
+    assert (alpha[1:cout:2] < 0).all() and (alpha[0:cout:2] > 0).all()
+    if k == 0:
+        got = _lib.ultra_conv0(img.to(dev), codes, alpha, shift, 4)
+    else:
+        x = codes_of(trace[k - 1]).to(torch.int8).to(dev)
+        got = _lib.ultra_conv(x, 3, codes, cout, 4, 4, alpha, shift, _lib.ULTRA_CODES_POOL if pool else _lib.ULTRA_CODES)
+    want = codes_of(trace[k])
+    assert_codes(got, want)
+    assert len(torch.unique(want[..., 1::2])) >= 6   # the decreasing channels spread their codes too
+
+
 @pytest.mark.parametrize("k", range(1, 8))
 def test_conv_block_stage_forced(dev, net, k):
     model, sd, img, trace, _, _ = net
@@ -109,6 +151,10 @@ def test_fused_network_end_to_end(dev, net):
     for got, want, want64 in ((gio, io, io64), (gp[0], p, p64)):
         floor = rel(want64, want)
         assert rel(got, want) <= max(1e-3, 2.5 * floor), (rel(got, want), floor)
+
+
+def test_decreasing_bn_fused_end_to_end(dev, net_decreasing):
+    test_fused_network_end_to_end(dev, net_decreasing)
 
 
 def test_module_api_vs_oracle(dev):
